@@ -1,0 +1,83 @@
+/*
+ * nart_hip.h — MI355X (gfx950) render path, C ABI.
+ *
+ * Replaces the reference's per-session hot path
+ *     std::vector<Pixel> RenderSession::Render() const      src/core/render.cpp:114-206
+ * (bucket loop + per-pixel RNG seed + Latin square + Camera::CastRay + Integrator::Li_alpha +
+ *  AddSample Gaussian splat + bucket-raster tile combine) with HIP kernels on one device.
+ * Li_alpha (src/integrators/pathintegrator.cpp:144-259) with its BVH traversal
+ * (src/core/bvh.cpp:132-176), BSDFs (src/core/bxdf.cpp, src/bxdfs/<name>.cpp), materials
+ * (src/materials/<type>material.cpp) and lights (src/lights/<type>light.cpp) run on the device.
+ *
+ * All entry points return NART_OK (0) or a negative NART_E_* code (nart_scene.h); no C++
+ * exception crosses the ABI and nothing aborts.  A context owns all device memory for one
+ * device and is not thread-safe (one caller thread, like the reference's main thread).
+ */
+#ifndef NART_HIP_H
+#define NART_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "nart_scene.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct nart_ctx nart_ctx;
+
+typedef struct nart_render_stats {
+    double render_ms;       /* wall time of the render call (host clock)               */
+    double kernel_ms;       /* device time of the path-tracing kernels (HIP events)     */
+    double splat_ms;        /* device time of the splat + combine kernels               */
+    uint32_t kernel_launches; /* number of path-tracing kernel launches timed in kernel_ms */
+    uint32_t reserved;
+    uint64_t samples;       /* camera samples counted in the metric (W*H*spp share)     */
+    uint64_t traced_samples;/* samples actually traced (incl. extra rows, render.cpp:164) */
+    /* Counter pass only (nart_hip_set_counters(ctx,1)); zero otherwise. */
+    uint64_t rays_extend, rays_shadow, node_visits, tri_tests, bounces;
+} nart_render_stats;
+
+/* Upload the scene, build the device BVH.  device_id: HIP ordinal. */
+int nart_hip_create(const nart_scene_blob* scene, int device_id, nart_ctx** out);
+void nart_hip_destroy(nart_ctx* ctx);
+const char* nart_hip_last_error(const nart_ctx* ctx);
+
+/* Whole-session render, Render()-equivalent: fills a caller-owned host buffer of
+   totalW*totalH nart_pixel (render.cpp:114-206 contract, render.h:18-21 layout). */
+int nart_hip_render(nart_ctx* ctx, const nart_render_params* p, nart_pixel* image,
+                    nart_render_stats* stats);
+
+/* Multi-GPU building block: render the listed buckets (bucket id = by*nBucketsX + bx) into
+   device-resident tiles d_tiles[i] (tile_size^2 nart_pixel each, same order as the list) on
+   `stream` (a hipStream_t, may be 0).  bucket_ids is a host array.  Asynchronous w.r.t. the
+   host except for small scratch uploads; synchronise the stream before reading d_tiles. */
+int nart_hip_render_buckets_async(nart_ctx* ctx, const nart_render_params* p,
+                                  const uint32_t* bucket_ids, uint32_t n_buckets,
+                                  nart_pixel* d_tiles, void* stream, nart_render_stats* stats);
+
+/* Device combine: d_tiles indexed by bucket id (all nBucketsX*nBucketsY tiles) into the
+   totalW*totalH device image, bucket raster order (render.cpp:183-203). */
+int nart_hip_combine_async(nart_ctx* ctx, const nart_render_params* p, const nart_pixel* d_tiles,
+                           nart_pixel* d_image, void* stream);
+
+/* Debug / parity: per-sample Li_alpha (float4) for pixels [x0,x0+w) x [y0,y0+h) in image
+   coordinates, all spp samples, into host out[((y-y0)*w + (x-x0))*spp + s][4]. */
+int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t x0, uint32_t y0,
+                            uint32_t w, uint32_t h, float* out);
+
+/* Enable the deterministic counter pass (node visits, triangle tests, rays) for the next
+   renders.  Slower; used to compute algorithmic bytes per sample. */
+int nart_hip_set_counters(nart_ctx* ctx, int enable);
+
+/* Device self-test: glibc-equivalent sinf/cosf over n inputs (parity of the device libm). */
+int nart_hip_eval_sincos(nart_ctx* ctx, const float* x, uint32_t n, float* sin_out, float* cos_out);
+
+/* Kernel variant: 0 = megakernel (one lane per pixel slot), 1 = wavefront (ray queues). */
+int nart_hip_set_variant(nart_ctx* ctx, int variant);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

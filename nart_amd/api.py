@@ -1,0 +1,293 @@
+"""ctypes bindings of the nart_amd C ABI (include/nart_scene.h, include/nart_hip.h).
+
+Mirrors the reference's host surface for the render path:
+    Scene(path)                        <- Scene::Scene (src/core/scene.cpp:3-26)
+    parse_args(argv) / load_sessions   <- ParseRenderParamArguments / LoadSessions (render.cpp:236-414)
+    HipRenderer(scene).render(params)  <- RenderSession::Render (render.cpp:114-206), on the GPU
+    write_exr(path, params, image)     <- RenderSession::WriteImageToEXR (render.cpp:208-234)
+The render path has no CPU fallback: without the HIP library (or a GPU) it raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(_HERE, "lib")
+
+NART_OK = 0
+ERRORS = {-1: "NART_E_INVALID", -2: "NART_E_IO", -3: "NART_E_HIP", -4: "NART_E_OOM", -5: "NART_E_RCCL",
+          -6: "NART_E_UNSUPPORTED"}
+
+PIXEL_FLOATS = 5  # struct Pixel { vec4 contribution; float filterWeightSum; } (render.h:18-21)
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+class NartError(RuntimeError):
+    def __init__(self, code, msg=""):
+        super().__init__("%s (%d)%s" % (ERRORS.get(code, "error"), code, (": " + msg) if msg else ""))
+        self.code = code
+
+
+class RenderParams(ctypes.Structure):
+    """struct RenderParams (include/nart/core/scene.h:25-36)."""
+    _fields_ = [("integrator", ctypes.c_int32), ("image_width", ctypes.c_uint32), ("image_height", ctypes.c_uint32),
+                ("bucket_size", ctypes.c_uint32), ("spp", ctypes.c_uint32), ("bounces", ctypes.c_uint32),
+                ("filter_width", ctypes.c_float), ("roughening_factor", ctypes.c_float)]
+
+    def __repr__(self):
+        return "RenderParams(%s)" % ", ".join("%s=%r" % (f, getattr(self, f)) for f, _ in self._fields_)
+
+    def copy(self):
+        p = RenderParams()
+        ctypes.pointer(p)[0] = self
+        return p
+
+
+class SessionGeometry(ctypes.Structure):
+    _fields_ = [("filter_bounds", ctypes.c_uint32), ("tile_size", ctypes.c_uint32), ("total_width", ctypes.c_uint32),
+                ("total_height", ctypes.c_uint32), ("n_buckets_x", ctypes.c_uint32), ("n_buckets_y", ctypes.c_uint32)]
+
+
+class RenderStats(ctypes.Structure):
+    _fields_ = [("render_ms", ctypes.c_double), ("kernel_ms", ctypes.c_double), ("splat_ms", ctypes.c_double),
+                ("kernel_launches", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("samples", ctypes.c_uint64),
+                ("traced_samples", ctypes.c_uint64), ("rays_extend", ctypes.c_uint64), ("rays_shadow", ctypes.c_uint64),
+                ("node_visits", ctypes.c_uint64), ("tri_tests", ctypes.c_uint64), ("bounces", ctypes.c_uint64)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+
+
+_P = ctypes.c_void_p
+_SCENE_SIGS = {
+    "nart_scene_load": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(_P)]),
+    "nart_scene_blob_of": (_P, [_P]),
+    "nart_scene_free": (None, [_P]),
+    "nart_scene_last_error": (ctypes.c_char_p, []),
+    "nart_render_params_init": (None, [ctypes.POINTER(RenderParams)]),
+    "nart_parse_args": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(RenderParams)]),
+    "nart_load_sessions": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(RenderParams), ctypes.POINTER(RenderParams),
+                                          ctypes.c_int]),
+    "nart_session_geometry_of": (None, [ctypes.POINTER(RenderParams), ctypes.POINTER(SessionGeometry)]),
+    "nart_filter_table": (None, [ctypes.POINTER(ctypes.c_float)]),
+    "nart_combine_tiles": (None, [ctypes.POINTER(RenderParams), _P, _P]),
+    "nart_write_exr": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(RenderParams), _P, ctypes.c_int]),
+    "nart_float_to_half": (ctypes.c_uint16, [ctypes.c_float]),
+    "nart_half_to_float": (ctypes.c_float, [ctypes.c_uint16]),
+    "nart_read_exr_rgba": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32),
+                                          ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(_P)]),
+    "nart_free": (None, [_P]),
+}
+_HIP_SIGS = {
+    "nart_hip_create": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_P)]),
+    "nart_hip_destroy": (None, [_P]),
+    "nart_hip_last_error": (ctypes.c_char_p, [_P]),
+    "nart_hip_render": (ctypes.c_int, [_P, ctypes.POINTER(RenderParams), _P, ctypes.POINTER(RenderStats)]),
+    "nart_hip_render_buckets_async": (ctypes.c_int, [_P, ctypes.POINTER(RenderParams), ctypes.POINTER(ctypes.c_uint32),
+                                                     ctypes.c_uint32, _P, _P, ctypes.POINTER(RenderStats)]),
+    "nart_hip_combine_async": (ctypes.c_int, [_P, ctypes.POINTER(RenderParams), _P, _P, _P]),
+    "nart_hip_render_samples": (ctypes.c_int, [_P, ctypes.POINTER(RenderParams), ctypes.c_uint32, ctypes.c_uint32,
+                                               ctypes.c_uint32, ctypes.c_uint32, _P]),
+    "nart_hip_set_counters": (ctypes.c_int, [_P, ctypes.c_int]),
+    "nart_hip_eval_sincos": (ctypes.c_int, [_P, _P, ctypes.c_uint32, _P, _P]),
+    "nart_hip_set_variant": (ctypes.c_int, [_P, ctypes.c_int]),
+}
+SCENE_SYMBOLS = tuple(_SCENE_SIGS)
+HIP_SYMBOLS = tuple(_HIP_SIGS)
+
+_libs = {}
+
+
+def _load(name, sigs):
+    if name in _libs:
+        return _libs[name]
+    path = os.path.join(LIB_DIR, name)
+    if not os.path.exists(path):
+        raise NativeLibraryMissing("%s not built (run nart_amd/build.py or __graft_entry__.build())" % path)
+    lib = ctypes.CDLL(path)
+    for fn, (res, args) in sigs.items():
+        f = getattr(lib, fn)
+        f.restype = res
+        f.argtypes = args
+    _libs[name] = lib
+    return lib
+
+
+def scene_lib():
+    return _load("libnart_scene.so", _SCENE_SIGS)
+
+
+def hip_lib():
+    return _load("libnart_hip.so", _HIP_SIGS)
+
+
+def default_params():
+    p = RenderParams()
+    scene_lib().nart_render_params_init(ctypes.byref(p))
+    return p
+
+
+def parse_args(argv):
+    """ParseRenderParamArguments: argv = [prog, scene, out, flags...]."""
+    p = default_params()
+    arr = (ctypes.c_char_p * len(argv))(*[a.encode() for a in argv])
+    rc = scene_lib().nart_parse_args(len(argv), arr, ctypes.byref(p))
+    if rc != NART_OK:
+        raise NartError(rc, scene_lib().nart_scene_last_error().decode())
+    return p
+
+
+def load_sessions(path, cli=None):
+    """LoadSessions: renderSessions[] resolved against CLI overrides."""
+    lib = scene_lib()
+    cli = cli if cli is not None else default_params()
+    n = lib.nart_load_sessions(path.encode(), ctypes.byref(cli), None, 0)
+    if n < 0:
+        raise NartError(n, lib.nart_scene_last_error().decode())
+    out = (RenderParams * max(n, 1))()
+    lib.nart_load_sessions(path.encode(), ctypes.byref(cli), out, n)
+    return [out[i].copy() for i in range(n)]
+
+
+def session_geometry(p):
+    g = SessionGeometry()
+    scene_lib().nart_session_geometry_of(ctypes.byref(p), ctypes.byref(g))
+    return g
+
+
+def filter_table():
+    t = (ctypes.c_float * 64)()
+    scene_lib().nart_filter_table(t)
+    return np.ctypeslib.as_array(t).copy()
+
+
+def combine_tiles(p, tiles):
+    g = session_geometry(p)
+    tiles = np.ascontiguousarray(tiles, dtype=np.float32)
+    img = np.zeros((g.total_height, g.total_width, PIXEL_FLOATS), np.float32)
+    scene_lib().nart_combine_tiles(ctypes.byref(p), tiles.ctypes.data, img.ctypes.data)
+    return img
+
+
+def write_exr(path, p, image, compression=3):
+    image = np.ascontiguousarray(image, dtype=np.float32)
+    rc = scene_lib().nart_write_exr(path.encode(), ctypes.byref(p), image.ctypes.data, compression)
+    if rc != NART_OK:
+        raise NartError(rc, scene_lib().nart_scene_last_error().decode())
+
+
+def read_exr(path):
+    """RGBA halves as float32 array (H, W, 4)."""
+    lib = scene_lib()
+    w, h, ptr = ctypes.c_uint32(), ctypes.c_uint32(), _P()
+    rc = lib.nart_read_exr_rgba(path.encode(), ctypes.byref(w), ctypes.byref(h), ctypes.byref(ptr))
+    if rc != NART_OK:
+        raise NartError(rc, lib.nart_scene_last_error().decode())
+    n = w.value * h.value * 4
+    halves = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint16)), shape=(n,)).copy()
+    lib.nart_free(ptr)
+    return halves.view(np.float16).astype(np.float32).reshape(h.value, w.value, 4)
+
+
+class Scene:
+    """Scene::Scene(path): JSON + .geo + EXR ingestion into the flat nart_scene_blob."""
+
+    def __init__(self, path):
+        self.path = path
+        self._lib = scene_lib()
+        self._h = _P()
+        rc = self._lib.nart_scene_load(path.encode(), ctypes.byref(self._h))
+        if rc != NART_OK:
+            raise NartError(rc, self._lib.nart_scene_last_error().decode())
+        self.blob = self._lib.nart_scene_blob_of(self._h)
+
+    def counts(self):
+        c = ctypes.cast(self.blob, ctypes.POINTER(ctypes.c_uint32))
+        return {"triangles": c[0], "meshes": c[1], "materials": c[2], "lights": c[3], "textures": c[4]}
+
+    def close(self):
+        if self._h:
+            self._lib.nart_scene_free(self._h)
+            self._h = _P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class HipRenderer:
+    """nart_ctx: the scene resident on one GPU; Render()-equivalent entry points."""
+
+    def __init__(self, scene, device=0):
+        self._lib = hip_lib()
+        self.scene = scene
+        self.device = device
+        self._ctx = _P()
+        rc = self._lib.nart_hip_create(scene.blob, device, ctypes.byref(self._ctx))
+        if rc != NART_OK:
+            raise NartError(rc, "nart_hip_create failed on device %d" % device)
+
+    def _check(self, rc):
+        if rc != NART_OK:
+            raise NartError(rc, self._lib.nart_hip_last_error(self._ctx).decode())
+
+    def set_counters(self, on):
+        self._check(self._lib.nart_hip_set_counters(self._ctx, 1 if on else 0))
+
+    def render(self, p, stats=None):
+        """Whole session -> (totalH, totalW, 5) float32 image of Pixels (host)."""
+        g = session_geometry(p)
+        img = np.empty((g.total_height, g.total_width, PIXEL_FLOATS), np.float32)
+        st = stats if stats is not None else RenderStats()
+        self._check(self._lib.nart_hip_render(self._ctx, ctypes.byref(p), img.ctypes.data, ctypes.byref(st)))
+        return img
+
+    def render_buckets_async(self, p, bucket_ids, d_tiles_ptr, stream_ptr=0, stats=None):
+        ids = np.ascontiguousarray(bucket_ids, dtype=np.uint32)
+        st = stats if stats is not None else RenderStats()
+        self._check(self._lib.nart_hip_render_buckets_async(
+            self._ctx, ctypes.byref(p), ids.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), len(ids),
+            _P(d_tiles_ptr), _P(stream_ptr), ctypes.byref(st)))
+        return st
+
+    def combine_async(self, p, d_tiles_ptr, d_image_ptr, stream_ptr=0):
+        self._check(self._lib.nart_hip_combine_async(self._ctx, ctypes.byref(p), _P(d_tiles_ptr), _P(d_image_ptr),
+                                                     _P(stream_ptr)))
+
+    def render_samples(self, p, x0, y0, w, h):
+        out = np.empty((h, w, p.spp, 4), np.float32)
+        self._check(self._lib.nart_hip_render_samples(self._ctx, ctypes.byref(p), x0, y0, w, h, out.ctypes.data))
+        return out
+
+    def eval_sincos(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        s = np.empty_like(x)
+        c = np.empty_like(x)
+        self._check(self._lib.nart_hip_eval_sincos(self._ctx, x.ctypes.data, len(x), s.ctypes.data, c.ctypes.data))
+        return s, c
+
+    def close(self):
+        if self._ctx:
+            self._lib.nart_hip_destroy(self._ctx)
+            self._ctx = _P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def finalize(p, image):
+    """WriteImageToEXR's per-pixel result = contribution / filterWeightSum (render.cpp:213-222)."""
+    g = session_geometry(p)
+    fb = g.filter_bounds
+    crop = image[fb:fb + p.image_height, fb:fb + p.image_width]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return crop[..., :4] / crop[..., 4:5]

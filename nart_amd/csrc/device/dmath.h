@@ -1,0 +1,182 @@
+// Device arithmetic for the nart render path (gfx950).
+//
+// Every operation reproduces the reference's float semantics bit for bit:
+//  * GLM 0.9.9.8 scalar code paths (association order of dot/normalize/mat*vec, ternary
+//    min/max, abs(x) = x >= 0 ? x : -x, fract, mod, mix);
+//  * correctly rounded f32 division and sqrt (hipcc default
+//    -fhip-fp32-correctly-rounded-divide-sqrt) and no FMA contraction (-ffp-contract=off);
+//  * sinf/cosf are glibc 2.35's algorithm (sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c,
+//    sincosf.h: double-precision range reduction + polynomials), verified bit-exact against
+//    the host libm over every float in [-7, 7] (tests/test_libm_parity.py).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define ND __device__ __forceinline__
+#define NHD __host__ __device__ __forceinline__
+
+namespace nd {
+
+struct f2 { float x, y; };
+struct f3 { float x, y, z; };
+struct f4 { float x, y, z, w; };
+
+NHD f2 F2(float x, float y) { f2 r; r.x = x; r.y = y; return r; }
+NHD f3 F3(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
+NHD f4 F4(float x, float y, float z, float w) { f4 r; r.x = x; r.y = y; r.z = z; r.w = w; return r; }
+NHD f3 add(f3 a, f3 b) { return F3(a.x + b.x, a.y + b.y, a.z + b.z); }
+NHD f3 sub(f3 a, f3 b) { return F3(a.x - b.x, a.y - b.y, a.z - b.z); }
+NHD f3 mul(f3 a, f3 b) { return F3(a.x * b.x, a.y * b.y, a.z * b.z); }
+NHD f3 muls(f3 a, float s) { return F3(a.x * s, a.y * s, a.z * s); }
+NHD f3 divs(f3 a, float s) { return F3(a.x / s, a.y / s, a.z / s); }
+NHD f3 neg(f3 a) { return F3(-a.x, -a.y, -a.z); }
+NHD float dot(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+NHD float dot4(f4 a, f4 b) { return (a.x * b.x + a.y * b.y) + (a.z * b.z + a.w * b.w); }
+NHD f3 cross(f3 x, f3 y) { return F3(x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y); }
+NHD f3 normalize(f3 v) { float s = 1.f / sqrtf(dot(v, v)); return muls(v, s); }
+NHD f4 normalize4(f4 v) { float s = 1.f / sqrtf(dot4(v, v)); return F4(v.x * s, v.y * s, v.z * s, v.w * s); }
+NHD float gmin(float a, float b) { return (b < a) ? b : a; }
+NHD float gmax(float a, float b) { return (a < b) ? b : a; }
+NHD float gabs(float x) { return x >= 0.f ? x : -x; }
+NHD float gfract(float x) { return x - floorf(x); }
+NHD float gmod(float a, float b) { return a - b * floorf(a / b); }
+NHD float gmix(float x, float y, float a) { return x * (1.f - a) + y * a; }
+NHD float comp(f3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
+// row vector * glm::mat4 (m[c*4+r]): r_i = m[i][0]v0 + m[i][1]v1 + m[i][2]v2 + m[i][3]v3
+NHD f4 vec_mul_mat(f4 v, const float* m) {
+    f4 r;
+    r.x = ((m[0] * v.x + m[1] * v.y) + m[2] * v.z) + m[3] * v.w;
+    r.y = ((m[4] * v.x + m[5] * v.y) + m[6] * v.z) + m[7] * v.w;
+    r.z = ((m[8] * v.x + m[9] * v.y) + m[10] * v.z) + m[11] * v.w;
+    r.w = ((m[12] * v.x + m[13] * v.y) + m[14] * v.z) + m[15] * v.w;
+    return r;
+}
+NHD f3 xyz(f4 v) { return F3(v.x, v.y, v.z); }
+
+// static_cast<uint32_t>(float) as the reference's x86-64 build evaluates it
+// (cvttss2si to 64 bits, low 32 bits; NaN / out of range -> 0).
+NHD uint32_t f2u32(float f) {
+    if (f >= 0.f && f < 4294967296.f) return (uint32_t)f;
+    if (!(f > -9.2233715e18f && f < 9.2233715e18f)) return 0u;
+    return (uint32_t)(int64_t)f;
+}
+NHD uint8_t f2u8(float f) { return (uint8_t)f2u32(f); }
+
+// glm constants: genType(<double literal>)
+#define ND_PI ((float)3.14159265358979323846264338327950288)
+#define ND_TWO_PI ((float)6.28318530717958647692528676655900576)
+#define ND_ONE_OVER_PI ((float)0.318309886183790671537767526745028724)
+#define ND_ONE_OVER_TWO_PI ((float)0.159154943091895335768883763372514362)
+#define ND_EPS 1.1920928955078125e-07f
+#define ND_ONE_MINUS_EPS (1.f - 1.1920928955078125e-07f)
+
+// ---------------------------------------------------------------- glibc sinf / cosf
+struct SinCosT {
+    double sign[4];
+    double hpi_inv, hpi, c0, c1, c2, c3, c4, s1, s2, s3;
+};
+
+// __sincosf_table (glibc sysdeps/ieee754/flt-32/s_sincosf_data.c), !TOINT_INTRINSICS
+static __constant__ const SinCosT kSinCosT[2] = {
+    {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, 0x1p0, -0x1.ffffffd0c621cp-2,
+     0x1.55553e1068f19p-5, -0x1.6c087e89a359dp-10, 0x1.99343027bf8c3p-16, -0x1.555545995a603p-3,
+     0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13},
+    {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, -0x1p0, 0x1.ffffffd0c621cp-2,
+     -0x1.55553e1068f19p-5, 0x1.6c087e89a359dp-10, -0x1.99343027bf8c3p-16, -0x1.555545995a603p-3,
+     0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13}};
+ND const SinCosT* sincos_table(int k) { return &kSinCosT[k]; }
+ND uint32_t abstop12(float x) { return (__float_as_uint(x) >> 20) & 0x7ff; }
+ND float sinf_poly(double x, double x2, const SinCosT* p, int n) {
+    if ((n & 1) == 0) {
+        double x3 = x * x2;
+        double s1 = p->s2 + x2 * p->s3;
+        double x7 = x3 * x2;
+        double s = x + x3 * p->s1;
+        return (float)(s + x7 * s1);
+    }
+    double x4 = x2 * x2;
+    double c2 = p->c3 + x2 * p->c4;
+    double c1 = p->c0 + x2 * p->c1;
+    double x6 = x4 * x2;
+    double c = c1 + x4 * p->c2;
+    return (float)(c + x6 * c2);
+}
+ND double reduce_fast(double x, const SinCosT* p, int* np) {
+    double r = x * p->hpi_inv;
+    int n = ((int32_t)r + 0x800000) >> 24;
+    *np = n;
+    return x - n * p->hpi;
+}
+// Valid for |y| < 120 (the reference only evaluates angles in [0, 2*pi]); larger inputs
+// would need glibc's reduce_large, which the render path never reaches.
+ND float glibc_sinf(float y) {
+    double x = y;
+    const SinCosT* p = sincos_table(0);
+    const float pio4f = (float)0x1.921FB54442D18p-1;
+    if (abstop12(y) < abstop12(pio4f)) {
+        double s = x * x;
+        if (abstop12(y) < abstop12(0x1p-12f)) return y;
+        return sinf_poly(x, s, p, 0);
+    }
+    int n;
+    x = reduce_fast(x, p, &n);
+    double s = p->sign[n & 3];
+    if (n & 2) p = sincos_table(1);
+    return sinf_poly(x * s, x * x, p, n);
+}
+ND float glibc_cosf(float y) {
+    double x = y;
+    const SinCosT* p = sincos_table(0);
+    const float pio4f = (float)0x1.921FB54442D18p-1;
+    if (abstop12(y) < abstop12(pio4f)) {
+        double x2 = x * x;
+        if (abstop12(y) < abstop12(0x1p-12f)) return 1.0f;
+        return sinf_poly(x, x2, p, 1);
+    }
+    int n;
+    x = reduce_fast(x, p, &n);
+    double s = p->sign[n & 3];
+    if (n & 2) p = sincos_table(1);
+    return sinf_poly(x * s, x * x, p, n ^ 1);
+}
+
+// ---------------------------------------------------------------- RNG (rng.h:8-59)
+ND uint32_t xorshift(uint32_t y) {
+    y ^= (y << 13);
+    y ^= (y >> 17);
+    y ^= (y << 5);
+    return y;
+}
+ND float rng_float(uint32_t& y) {
+    y = xorshift(y);
+    float f = (float)(uint32_t)(y * 0x9E3779BBu) * 2.3283064365386963e-10f;
+    return gmin(ND_ONE_MINUS_EPS, f);
+}
+ND uint32_t rng_int(uint32_t& y, uint32_t max) {
+    y = xorshift(y);
+    return (uint32_t)(((uint64_t)(uint32_t)(y * 0x9E3779B9u) * ((uint64_t)max + 1)) >> 32);
+}
+
+// ---------------------------------------------------------------- sampling.cpp
+ND f2 uniform_sample_disk(f2 s) {  // sampling.cpp:5-16
+    float r = sqrtf(s.x);
+    float theta = s.y * ND_TWO_PI;
+    float c = glibc_cosf(theta), sn = glibc_sinf(theta);
+    return F2(r * c, r * sn);
+}
+ND f2 uniform_sample_ring(f2 s, float& pdf, float inner) {  // sampling.cpp:18-31
+    float r = sqrtf(gmix(inner, 1.f, s.x));
+    float theta = s.y * ND_TWO_PI;
+    float c = glibc_cosf(theta), sn = glibc_sinf(theta);
+    pdf = 1.f / (ND_PI * (1.f - inner));
+    return F2(r * c, r * sn);
+}
+ND f3 cosine_sample_hemisphere(f2 s, float& pdf) {  // sampling.cpp:47-58
+    f2 d = uniform_sample_disk(s);
+    float z = sqrtf(1.f - (d.x * d.x + d.y * d.y));
+    pdf = z * ND_ONE_OVER_PI;
+    return F3(d.x, d.y, z);
+}
+
+}  // namespace nd

@@ -1,0 +1,99 @@
+// Device-resident scene layout for the nart render path.  Built once per context by the
+// host (api.cpp) from the nart_scene_blob; every derived constant that the reference
+// recomputes per call (light frames, triangle normals) is precomputed on the host with the
+// identical float operations, so the device reads bit-identical values.
+//
+// HBM layout (all arrays 16-B aligned, read-only during a render):
+//   nodes     : BVH2, 64 B per node (two child AABBs + two child codes), depth-first order
+//   tri_isect : 64 B per triangle in BVH leaf order: {n.xyz, dot(v0,n)}, {v0.xyz, v1.x},
+//               {v1.yz, v2.xy}, {v2.z, global index, -, -}
+//   tris      : the reference's 96-B Triangle records in scene order (winner attributes)
+//   tri_mesh  : mesh id per triangle (scene order)
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../../include/nart_scene.h"
+
+namespace nd {
+
+// Child code: >= 0 inner node index; < 0 leaf = ~(first << 5 | (count - 1)).
+struct BVHNode {
+    float lo0[3], hi0[3];
+    float lo1[3], hi1[3];
+    int32_t child[2];
+    int32_t pad[2];
+};
+static_assert(sizeof(BVHNode) == 64, "BVHNode must be 64 B");
+
+#define NART_LEAF_MAX 32
+#define NART_STACK_DEPTH 20
+
+struct DPattern {
+    int32_t type;  // NART_PTN_*
+    int32_t tex;
+    int32_t rough;
+    float v[3];
+};
+
+struct DMaterial {
+    int32_t type;  // NART_MAT_*
+    int32_t has_normal;
+    DPattern rho_d, rho_s, tau, eta, alpha, normal;
+};
+
+// Light with the per-call constants of disklight.cpp / ringlight.cpp precomputed.
+struct DLight {
+    int32_t type;  // NART_LIGHT_*
+    float radius, inner, intensity;
+    DPattern Le;
+    float m[16];         // LightToWorld (glm storage)
+    float center[3];     // vec3(vec4(0,0,0,1) * M)
+    float n[3];          // vec3(vec4(0,0,-1,0) * M)
+    float D;             // dot(center, n)
+    float axu[4];        // vec4(1,0,0,0) * M
+    float axv[4];        // vec4(0,1,0,0) * M
+    float pdf_area;      // 1/(pi r r) (disk) or 1/(pi (1 - ri^2/r^2) r r) (ring)
+    float r2, ri2;       // radius^2, innerRadius^2
+    float inner_ratio;   // innerRadius / radius
+    int32_t env;         // index into env distribution table, -1 if none
+};
+
+struct DTexture {
+    uint32_t w, h;
+    uint64_t offset;  // into tex_pool (halves, RGBA)
+};
+
+// Piecewise2DDistribution (texturepattern.cpp:3-109) for a texture-lit environment light.
+struct DEnvDist {
+    uint32_t w, h;
+    float invW, invH;
+    const float *mpdf, *cpdf, *mcdf, *ccdf;
+};
+
+struct DMesh {
+    uint32_t material;
+    uint32_t priority;
+};
+
+struct DScene {
+    const BVHNode* nodes;
+    const float4* tri_isect;
+    const nart_triangle* tris;
+    const uint32_t* tri_mesh;
+    const DMesh* meshes;
+    const DMaterial* mats;
+    const DLight* lights;
+    const DTexture* texs;
+    const uint16_t* tex_pool;
+    const DEnvDist* envs;
+    uint32_t num_lights;
+    uint32_t num_tris;
+    int32_t root;            // root code (inner node index or leaf code)
+    int32_t geometry_visible;// 0 when the reference octree's root is a leaf (bvh.cpp:131, Q14)
+    float cam_m[16];
+    float cam_tan;           // tan(radians(fov)) (host libm, as the reference)
+};
+
+}  // namespace nd

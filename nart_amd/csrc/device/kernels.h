@@ -1,0 +1,492 @@
+// Kernels of the nart render path (gfx950):
+//   k_latin    per traced pixel: RNG seed + LatinSquare            (render.cpp:81-85, sampling.cpp:72-86)
+//   k_render   per traced pixel: all spp samples of Li_alpha       (render.cpp:87-107, pathintegrator.cpp)
+//   k_splat    per bucket tile pixel: ordered Gaussian splat      (render.cpp:23-70)
+//   k_combine  per image pixel: tiles summed in bucket raster order (render.cpp:183-203)
+#pragma once
+
+#include "path.h"
+
+namespace nd {
+
+// ---------------------------------------------------------------- nested-dielectric list
+// IntersectionInfo list (pathintegrator.h:9-19, pathintegrator.cpp:7-36, 123-142), kept in
+// registers: every access is an unrolled compare/select over MAXL slots (no dynamic indexing).
+template <int MAXL>
+struct IList {
+    uint32_t id[MAXL];  // meshID (24 bit) | priority << 24
+    float eta[MAXL];
+    uint32_t n;
+
+    ND bool valid(uint32_t meshID, uint32_t prio, float& eta_outer) const {
+        eta_outer = 1.f;
+        uint32_t lastId = 0;
+        float lastEta = 1.f, penEta = 1.f;
+        bool ok = true;
+#pragma unroll
+        for (int k = 0; k < MAXL; ++k) {
+            if (k + 1 == (int)n) {
+                lastId = id[k] & 0xFFFFFFu;
+                lastEta = eta[k];
+            }
+            if (k + 2 == (int)n) penEta = eta[k];
+            if (k < (int)n && (prio & 0xFFu) < (id[k] >> 24)) ok = false;
+        }
+        if (n) {
+            if (lastId != meshID) eta_outer = lastEta;
+            else if (n >= 2) eta_outer = penEta;
+        }
+        return ok;
+    }
+    ND void update(uint32_t meshID, uint32_t prio, float eta_s) {
+        int found = -1;
+#pragma unroll
+        for (int k = 0; k < MAXL; ++k)
+            if (k < (int)n && (id[k] & 0xFFFFFFu) == meshID) found = k;  // most recent match
+        if (found >= 0) {
+#pragma unroll
+            for (int j = 0; j + 1 < MAXL; ++j) {
+                if (j >= found && j + 1 < (int)n) {
+                    id[j] = id[j + 1];
+                    eta[j] = eta[j + 1];
+                }
+            }
+            --n;
+        } else {
+#pragma unroll
+            for (int k = 0; k < MAXL; ++k) {
+                if (k == (int)n) {
+                    id[k] = (meshID & 0xFFFFFFu) | ((prio & 0xFFu) << 24);
+                    eta[k] = eta_s;
+                }
+            }
+            ++n;
+        }
+    }
+};
+
+// ---------------------------------------------------------------- camera (pinholecamera.cpp:9-40)
+ND Ray cast_ray(const DScene& S, f2 smp, uint32_t W, uint32_t H, uint32_t x, uint32_t y) {
+    float aspect = (float)W / (float)H;
+    float px = ((((float)x + smp.x) / (float)W) * 2.f - 1.f) * S.cam_tan * aspect;
+    float py = ((((float)y + smp.y) / (float)H) * -2.f + 1.f) * S.cam_tan;
+    f4 d = normalize4(F4(px, py, -1.f, 0.f));
+    f4 o = vec_mul_mat(F4(0.f, 0.f, 0.f, 1.f), S.cam_m);
+    d = vec_mul_mat(d, S.cam_m);
+    return make_ray(xyz(o), xyz(d));
+}
+
+struct RenderArgs {
+    const uint32_t* slot_xy;  // traced pixel (x | y << 16) in image coordinates
+    const float2* samples;    // [slot][spp] LatinSquare image samples
+    const uint32_t* rng0;     // [slot] RNG state after the LatinSquare
+    float4* Lout;             // [slot][spp] Li_alpha
+    uint32_t n_slots, spp, bounces, W, H, totalW, stack_depth;
+    float gamma;              // roughening factor squared (pathintegrator.cpp:163)
+    unsigned long long* counters;  // [5] extend rays, shadow rays, node visits, tri tests, bounces
+};
+
+// ---------------------------------------------------------------- LatinSquare per pixel
+__global__ __launch_bounds__(256) void k_latin(RenderArgs A) {
+    uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot >= A.n_slots) return;
+    uint32_t xy = A.slot_xy[slot];
+    uint32_t x = xy & 0xFFFFu, y = xy >> 16;
+    uint32_t rng = (y * A.totalW + x) + 2463534242u;  // RNG::Seed (rng.h:10-13)
+    float2* s = const_cast<float2*>(A.samples) + (size_t)slot * A.spp;
+    const uint32_t n = A.spp;
+    const float inv = 1.f / (float)n;
+    for (uint32_t i = 0; i < n; ++i) {
+        float a = ((float)i + rng_float(rng)) * inv;  // StratifiedSample1D, x drawn first (Q2)
+        float b = ((float)i + rng_float(rng)) * inv;
+        s[i] = make_float2(a, b);
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t c = rng_int(rng, n - 1 - i);
+        float t = s[i].x;
+        s[i].x = s[c].x;
+        s[c].x = t;
+        c = rng_int(rng, n - 1 - i);
+        t = s[i].y;
+        s[i].y = s[c].y;
+        s[c].y = t;
+    }
+    const_cast<uint32_t*>(A.rng0)[slot] = rng;
+}
+
+enum { ST_EXT = 0, ST_SH1 = 1, ST_SH2 = 2 };
+
+// ---------------------------------------------------------------- path tracing megakernel
+// One lane per traced pixel; the lane walks its pixel's spp samples in order on one RNG
+// stream.  Each loop iteration traces exactly one ray (extension or shadow) through the
+// shared traversal loop, then advances the lane's path state machine; a lane whose path
+// ends starts its next sample immediately (path regeneration), so lanes of a wave stay busy.
+template <int MAXL, bool COUNT>
+__global__ __launch_bounds__(256) void k_render(DScene S, RenderArgs A) {
+    // LDS traversal stack: stack_depth entries of (node code, entry distance) per lane,
+    // laid out [depth][lane] so a wave's 64 lanes hit 64 distinct banks.
+    extern __shared__ __attribute__((aligned(16))) int s_dyn[];
+    int* s_code = s_dyn;
+    float* s_tn = reinterpret_cast<float*>(s_dyn + A.stack_depth * blockDim.x);
+    const int tid = threadIdx.x;
+    const uint32_t slot = blockIdx.x * blockDim.x + tid;
+    if (slot >= A.n_slots) return;
+    const uint32_t xy = A.slot_xy[slot];
+    const uint32_t px = xy & 0xFFFFu, py = xy >> 16;
+    uint32_t rng = A.rng0[slot];
+    const float2* smp = A.samples + (size_t)slot * A.spp;
+    float4* out = A.Lout + (size_t)slot * A.spp;
+    int* sc = s_code + tid;
+    float* stn = s_tn + tid;
+    const int stride = blockDim.x;
+    const float nL = (float)S.num_lights;
+    TraceCounters cnt = {0u, 0u};
+    uint32_t n_ext = 0, n_sh = 0, n_bounce = 0;
+
+    uint32_t s = 0;
+    f3 L, beta, Le, c1, c2, betak, Led;
+    float alpha = 0.f, eta_sampled = 1.f, eta_outer = 1.f, alphaTweak = 1.f;
+    uint32_t flags = 0, bounce = 0;
+    IList<MAXL> list;
+    list.n = 0;
+    Ray ray, cur, nxt, sh2;
+    float tmax = 0.f, sh2max = 0.f;
+    int stage = ST_EXT;
+    bool lightHit = false, use1 = false, use2 = false, cont = false, have_ed = false;
+    bool new_sample = true, new_bounce = false;
+
+    for (;;) {
+        if (new_sample) {
+            if (s >= A.spp) break;
+            float2 sm = smp[s];
+            ray = cast_ray(S, F2(sm.x, sm.y), A.W, A.H, px, py);
+            L = F3(0.f, 0.f, 0.f);
+            alpha = 0.f;
+            eta_sampled = 1.f;
+            eta_outer = 1.f;
+            beta = F3(1.f, 1.f, 1.f);
+            flags = 0;
+            alphaTweak = 1.f;
+            bounce = 0;
+            list.n = 0;
+            new_sample = false;
+            new_bounce = true;
+        }
+        if (new_bounce) {
+            new_bounce = false;
+            if (bounce >= A.bounces) {
+                out[s] = make_float4(L.x, L.y, L.z, alpha);
+                ++s;
+                new_sample = true;
+                continue;
+            }
+            // light intersections (pathintegrator.cpp:167-182)
+            float lightTMax = __builtin_inff();
+            lightHit = false;
+            Le = F3(0.f, 0.f, 0.f);
+            for (uint32_t j = 0; j < S.num_lights; ++j) {
+                float lt = __builtin_inff();
+                f3 Li = light_li(S, S.lights[j], ray.o, ray.d, nullptr, lt);
+                if (lt < lightTMax) {
+                    Le = Li;
+                    lightTMax = lt;
+                    lightHit = true;
+                    alpha = 1.f;
+                }
+            }
+            cur = ray;
+            tmax = lightTMax;
+            stage = ST_EXT;
+            if (COUNT) { ++n_ext; ++n_bounce; }
+        }
+
+        float bt;
+        uint32_t bg;
+        const bool hit = traverse<COUNT>(S, cur, tmax, stage != ST_EXT, bt, bg, sc, stn, stride, cnt);
+
+        bool resolve = false;
+        if (stage == ST_EXT) {
+            if (!hit) {
+                // escaped: at bounce 0 the light seen directly is the result; at bounce > 0 the
+                // reference repeats the same miss until the loop ends (no RNG, no state change)
+                if (bounce == 0 && lightHit) L = Le;
+                out[s] = make_float4(L.x, L.y, L.z, alpha);
+                ++s;
+                new_sample = true;
+                continue;
+            }
+            Isect is;
+            fill_isect(S, cur, bg, is);
+            BSDF bsdf;
+            create_bsdf(S, is, alphaTweak, bsdf);
+            use1 = use2 = false;
+            if (list.valid(is.meshID, is.priority, eta_outer)) {
+                if (bounce == 0) alpha = 1.f;
+                const f3 wo = to_local(bsdf, neg(cur.d));
+                // ---- EstimateDirect (pathintegrator.cpp:38-121)
+                const DLight& Lg = S.lights[f2u8(gmin(rng_float(rng), ND_ONE_MINUS_EPS) * nL)];
+                float sPdf = 0.f, lPdf = 0.f;
+                float sx = rng_float(rng);
+                float sy = rng_float(rng);
+                float bsmp = rng_float(rng);
+                uint32_t dflags = 0;
+                f3 wi;
+                f3 f = bsdf_sample_f(bsdf, wo, wi, bsmp, F2(sx, sy), sPdf, dflags, true, eta_outer, nullptr, nullptr);
+                if (sPdf > 0.f) {
+                    float flip = wi.z > 0.f ? 1.f : -1.f;
+                    f3 wW = to_world(bsdf, wi);
+                    float lt = __builtin_inff();
+                    f3 Li = light_li(S, Lg, is.p, wW, &lPdf, lt);
+                    float weight = 1.f;
+                    bool add1 = true;
+                    if (!(dflags & F_SPECULAR)) {
+                        weight = (sPdf * sPdf) / (sPdf * sPdf + lPdf * lPdf);
+                        add1 = lPdf > 0.f;
+                    }
+                    if (add1) {
+                        c1 = divs(muls(muls(mul(f, Li), gabs(wi.z)), weight), sPdf);
+                        // an all-zero term cannot change the sum: skip its shadow ray
+                        use1 = !(c1.x == 0.f && c1.y == 0.f && c1.z == 0.f);
+                        if (use1) {
+                            cur = make_ray(add(is.p, muls(muls(is.gn, SHADOW_BIAS), flip)), wW);
+                            tmax = lt;
+                        }
+                    }
+                }
+                lPdf = 0.f;
+                float lx = rng_float(rng);
+                float ly = rng_float(rng);
+                f3 wiW;
+                float lt2 = __builtin_inff();
+                f3 Li2 = light_sample_li(S, Lg, is.p, wiW, F2(lx, ly), lPdf, lt2);
+                f3 wi2 = to_local(bsdf, wiW);
+                if (lPdf > 0.f) {
+                    float sp2 = bsdf_pdf(bsdf, wo, wi2, true, eta_outer);
+                    if (sp2 > 0.f) {
+                        f3 fv = bsdf_f(bsdf, wo, wi2, true, eta_outer);
+                        float weight = (lPdf * lPdf) / (sp2 * sp2 + lPdf * lPdf);
+                        c2 = divs(muls(muls(mul(fv, Li2), gabs(wi2.z)), weight), lPdf);
+                        use2 = !(c2.x == 0.f && c2.y == 0.f && c2.z == 0.f);
+                        if (use2) {
+                            float flip2 = wi2.z > 0.f ? 1.f : -1.f;
+                            sh2 = make_ray(add(is.p, muls(muls(is.gn, SHADOW_BIAS), flip2)), wiW);
+                            sh2max = lt2;
+                        }
+                    }
+                }
+                betak = beta;
+                have_ed = true;
+                // ---- continuation (pathintegrator.cpp:199-220)
+                float a = rng_float(rng);
+                float b = rng_float(rng);
+                float bs2 = rng_float(rng);
+                float cpdf = 0.f, alpha_i = 0.f;
+                f3 wic;
+                f3 fc = bsdf_sample_f(bsdf, wo, wic, bs2, F2(a, b), cpdf, flags, false, eta_outer, &alpha_i,
+                                      &eta_sampled);
+                if (cpdf <= 0.f) {
+                    cont = false;
+                } else {
+                    alphaTweak = (1.f - (A.gamma * alpha_i)) * alphaTweak;
+                    beta = mul(beta, muls(divs(fc, cpdf), gabs(wic.z)));
+                    float flip = wic.z > 0.f ? 1.f : -1.f;
+                    nxt = make_ray(add(is.p, muls(muls(is.gn, SHADOW_BIAS), flip)), to_world(bsdf, wic));
+                    cont = true;
+                }
+            } else {
+                // lower-priority interface: step through (pathintegrator.cpp:223-229)
+                nxt = make_ray(add(is.p, muls(cur.d, SHADOW_BIAS)), cur.d);
+                flags = F_TRANSMISSIVE;
+                float bs2 = rng_float(rng);
+                eta_sampled = bsdf_sample_eta(bsdf, bs2);
+                cont = true;
+                have_ed = false;
+            }
+            if (cont) {
+                if (flags & F_TRANSMISSIVE) list.update(is.meshID, is.priority, eta_sampled);
+                // Russian roulette (pathintegrator.cpp:236-246)
+                float q = gmax((beta.x + beta.y + beta.z) * 0.33333f, 0.f);
+                if (bounce > 3) {
+                    if (q >= rng_float(rng)) beta = divs(beta, q);
+                    else cont = false;
+                }
+            }
+            ++bounce;
+            Led = F3(0.f, 0.f, 0.f);
+            if (use1) {
+                stage = ST_SH1;
+                if (COUNT) ++n_sh;
+            } else if (use2) {
+                stage = ST_SH2;
+                cur = sh2;
+                tmax = sh2max;
+                if (COUNT) ++n_sh;
+            } else {
+                resolve = true;
+            }
+        } else if (stage == ST_SH1) {
+            if (!hit) Led = add(Led, c1);
+            if (use2) {
+                stage = ST_SH2;
+                cur = sh2;
+                tmax = sh2max;
+                if (COUNT) ++n_sh;
+            } else {
+                resolve = true;
+            }
+        } else {
+            if (!hit) Led = add(Led, c2);
+            resolve = true;
+        }
+
+        if (resolve) {
+            // L += EstimateDirect(...) * beta, with EstimateDirect = ((0 + c1) + c2) * numLights
+            if (have_ed) L = add(L, mul(muls(Led, nL), betak));
+            if (cont) {
+                ray = nxt;
+                new_bounce = true;
+            } else {
+                out[s] = make_float4(L.x, L.y, L.z, alpha);
+                ++s;
+                new_sample = true;
+            }
+        }
+    }
+    if (COUNT) {
+        atomicAdd(&A.counters[0], (unsigned long long)n_ext);
+        atomicAdd(&A.counters[1], (unsigned long long)n_sh);
+        atomicAdd(&A.counters[2], (unsigned long long)cnt.nodes);
+        atomicAdd(&A.counters[3], (unsigned long long)cnt.tris);
+        atomicAdd(&A.counters[4], (unsigned long long)n_bounce);
+    }
+}
+
+// ---------------------------------------------------------------- splat (gather form)
+struct SplatArgs {
+    const uint32_t* bucket_ids;   // [n_buckets] bucket id = by * nbx + bx
+    const uint32_t* bucket_base;  // [n_buckets] first slot of each bucket
+    const float2* samples;        // [slot][spp]
+    const float4* Lout;           // [slot][spp]
+    float* tiles;                 // [n_buckets][tile*tile][5] (nart_pixel AoS)
+    const float* table;           // [64] Gaussian filter table
+    uint32_t n_buckets, spp, B, fb, tile, nbx, totalW, totalH;
+    float fw;
+};
+
+// Exact AddSample test: does this sample's splat loop (render.cpp:27-68) visit tile pixel
+// (tx, ty)?  If so, return the filter weight it adds there.
+ND bool splat_hits(const SplatArgs& A, float scx, float scy, uint32_t tx, uint32_t ty, float& w) {
+    const float fw = A.fw, fb = (float)A.fb, Bf = (float)A.B;
+    uint32_t x0 = f2u32(floorf(scx - fw)), x1 = f2u32(ceilf(scx + fw));
+    uint32_t y0 = f2u32(floorf(scy - fw)), y1 = f2u32(ceilf(scy + fw));
+    float mx = gmod(scx - fb, Bf), my = gmod(scy - fb, Bf);
+    // tileX(x) = floor(((x + 0.5) - scx) + mx + fb) is x - const for all x of the loop;
+    // solve for x, then verify exactly.
+    float dx0 = ((float)x0 + 0.5f) - scx;
+    uint32_t t0 = f2u32(floorf(dx0 + mx + fb));
+    uint32_t xs = x0 + (tx - t0);
+    if (xs < x0 || xs >= x1) return false;
+    float distX = ((float)xs + 0.5f) - scx;
+    if (f2u32(floorf(distX + mx + fb)) != tx) return false;
+    float dy0 = ((float)y0 + 0.5f) - scy;
+    uint32_t u0 = f2u32(floorf(dy0 + my + fb));
+    uint32_t ys = y0 + (ty - u0);
+    if (ys < y0 || ys >= y1) return false;
+    float distY = ((float)ys + 0.5f) - scy;
+    if (f2u32(floorf(distY + my + fb)) != ty) return false;
+    float dist = sqrtf(distX * distX + distY * distY);
+    uint32_t fi = f2u8((dist / fw) * 64);
+    fi = (63u < fi) ? 63u : fi;
+    w = A.table[fi];
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_splat(SplatArgs A) {
+    const uint32_t tpx = A.tile * A.tile;
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (uint64_t)A.n_buckets * tpx) return;
+    const uint32_t bi = (uint32_t)(gid / tpx), tp = (uint32_t)(gid % tpx);
+    const uint32_t tx = tp % A.tile, ty = tp / A.tile;
+    const uint32_t bid = A.bucket_ids[bi];
+    const uint32_t bx = bid % A.nbx, by = bid / A.nbx;
+    const uint32_t x0 = A.B * bx, y0 = A.B * by;
+    const uint32_t x1 = min(A.B * (bx + 1), A.totalW), y1 = min(A.B * (by + 1), A.totalH);
+    const int bw = (int)(x1 - x0), bh = (int)(y1 - y0);
+    const uint32_t base = A.bucket_base[bi];
+    const int r = (int)ceilf(A.fw) + 2;
+    // candidate source pixels: geometric neighbourhood plus the last row/column, whose
+    // samples can wrap onto the next bucket's origin through glm::mod (render.cpp:52-61)
+    const int sxlo = max(0, (int)tx - (int)A.fb - r), sxhi = min(bw - 1, (int)tx - (int)A.fb + r);
+    const int sylo = max(0, (int)ty - (int)A.fb - r), syhi = min(bh - 1, (int)ty - (int)A.fb + r);
+    float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f, ws = 0.f;
+    const int nrow = (syhi >= sylo ? syhi - sylo + 1 : 0) + (bh - 1 > syhi ? 1 : 0);
+    const int ncol = (sxhi >= sxlo ? sxhi - sxlo + 1 : 0) + (bw - 1 > sxhi ? 1 : 0);
+    for (int ri = 0; ri < nrow; ++ri) {
+        const int sy = (sylo + ri <= syhi) ? sylo + ri : bh - 1;
+        const float fy = (float)(y0 + (uint32_t)sy + A.fb);
+        for (int ci = 0; ci < ncol; ++ci) {
+            const int sx = (sxlo + ci <= sxhi) ? sxlo + ci : bw - 1;
+            const float fx = (float)(x0 + (uint32_t)sx + A.fb);
+            const uint64_t slot = base + (uint64_t)sy * bw + sx;
+            const float2* sp = A.samples + slot * A.spp;
+            const float4* lp = A.Lout + slot * A.spp;
+            for (uint32_t i = 0; i < A.spp; ++i) {
+                float2 uv = sp[i];
+                float w;
+                if (splat_hits(A, fx + uv.x, fy + uv.y, tx, ty, w)) {
+                    float4 Lv = lp[i];
+                    c0 += Lv.x * w;
+                    c1 += Lv.y * w;
+                    c2 += Lv.z * w;
+                    c3 += Lv.w * w;
+                    ws += w;
+                }
+            }
+        }
+    }
+    float* o = A.tiles + ((uint64_t)bi * tpx + tp) * 5;
+    o[0] = c0;
+    o[1] = c1;
+    o[2] = c2;
+    o[3] = c3;
+    o[4] = ws;
+}
+
+// ---------------------------------------------------------------- combine
+struct CombineArgs {
+    const float* tiles;  // [bucket id][tile*tile][5]
+    float* image;        // [totalH][totalW][5]
+    uint32_t W, H, B, fb, tile, nbx, nby, totalW, totalH;
+};
+__global__ __launch_bounds__(256) void k_combine(CombineArgs A) {
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (uint64_t)A.totalW * A.totalH) return;
+    const uint32_t pX = (uint32_t)(gid % A.totalW), pY = (uint32_t)(gid / A.totalW);
+    float c[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    if (pX < A.W + A.fb && pY < A.H + A.fb) {
+        const uint32_t ilo = pX + 1 > A.tile ? (pX + 1 - A.tile + A.B - 1) / A.B : 0;
+        const uint32_t ihi = min(pX / A.B, A.nbx - 1);
+        const uint32_t jlo = pY + 1 > A.tile ? (pY + 1 - A.tile + A.B - 1) / A.B : 0;
+        const uint32_t jhi = min(pY / A.B, A.nby - 1);
+        for (uint32_t j = jlo; j <= jhi; ++j)
+            for (uint32_t i = ilo; i <= ihi; ++i) {
+                const float* t = A.tiles + ((uint64_t)(j * A.nbx + i) * A.tile * A.tile +
+                                            (uint64_t)(pY - j * A.B) * A.tile + (pX - i * A.B)) * 5;
+#pragma unroll
+                for (int k = 0; k < 5; ++k) c[k] += t[k];
+            }
+    }
+    float* o = A.image + gid * 5;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) o[k] = c[k];
+}
+
+// ---------------------------------------------------------------- libm self-test
+__global__ void k_sincos(const float* x, uint32_t n, float* s, float* c) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    s[i] = glibc_sinf(x[i]);
+    c[i] = glibc_cosf(x[i]);
+}
+
+}  // namespace nd

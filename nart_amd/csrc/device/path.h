@@ -1,0 +1,648 @@
+// Device path integrator for nart (gfx950).  Mirrors, function by function and operation by
+// operation, src/integrators/pathintegrator.cpp, src/core/{geometry,bxdf}.cpp,
+// src/bxdfs/*, src/materials/*, src/lights/{disk,ring,environment}light.cpp,
+// src/patterns/*, src/cameras/pinholecamera.cpp.  Only the acceleration structure differs:
+// the reference's octree of triangle chunks (bvh.cpp) is replaced by a binned-SAH BVH2 that
+// returns the same closest hit (ties broken by scene order).
+#pragma once
+
+#include "dmath.h"
+#include "dscene.h"
+
+namespace nd {
+
+enum { F_SPECULAR = 1, F_GLOSSY = 2, F_DIFFUSE = 4, F_TRANSMISSIVE = 8 };
+#define SHADOW_BIAS 0.001f
+#define NO_HIT 0xFFFFFFFFu
+
+// ---------------------------------------------------------------- Ray (geometry.cpp:3-15)
+struct Ray {
+    f3 o, d;
+    int major;
+    float Sx, Sy, Sz;
+};
+ND Ray make_ray(f3 o, f3 d) {
+    Ray r;
+    r.o = o;
+    r.d = d;
+    f3 a = F3(gabs(d.x), gabs(d.y), gabs(d.z));
+    r.major = (a.x > a.y) ? ((a.x > a.z) ? 0 : 2) : ((a.y > a.z) ? 1 : 2);
+    int m0 = r.major + 1;
+    if (m0 == 3) m0 = 0;
+    int m1 = r.major + 2;
+    if (m1 >= 3) m1 -= 3;
+    r.Sz = 1.f / comp(d, r.major);
+    r.Sx = -comp(d, m0) * r.Sz;
+    r.Sy = -comp(d, m1) * r.Sz;
+    return r;
+}
+// (p[m0], p[m1], p[major]) permutation of Triangle::Intersect (geometry.cpp:48-56)
+ND f3 permute(f3 p, int major) {
+    if (major == 0) return F3(p.y, p.z, p.x);
+    if (major == 1) return F3(p.z, p.x, p.y);
+    return p;
+}
+
+// Sheared-space edge functions (geometry.cpp:42-75)
+ND void edge_functions(const Ray& r, f3 v0, f3 v1, f3 v2, float& e0, float& e1, float& e2) {
+    f3 p0 = permute(sub(v0, r.o), r.major);
+    f3 p1 = permute(sub(v1, r.o), r.major);
+    f3 p2 = permute(sub(v2, r.o), r.major);
+    p0.x += p0.z * r.Sx;
+    p0.y += p0.z * r.Sy;
+    p1.x += p1.z * r.Sx;
+    p1.y += p1.z * r.Sy;
+    p2.x += p2.z * r.Sx;
+    p2.y += p2.z * r.Sy;
+    e0 = (p1.x * p2.y) - (p1.y * p2.x);
+    e1 = (p2.x * p0.y) - (p2.y * p0.x);
+    e2 = (p0.x * p1.y) - (p0.y * p1.x);
+}
+ND bool edges_accept(float e0, float e1, float e2) {  // geometry.cpp:78-81
+    if ((e0 < 0 || e1 < 0 || e2 < 0) && (e0 > 0 || e1 > 0 || e2 > 0)) return false;
+    if (gabs(e0) + gabs(e1) + gabs(e2) == 0.f) return false;
+    return true;
+}
+
+// ---------------------------------------------------------------- BVH traversal
+struct TraceCounters {
+    uint32_t nodes, tris;
+};
+
+// Closest hit (ANY=false): minimum (t, scene index) over triangles with 0 < t < tmax whose
+// sheared edge test passes -- the set Octree::Intersect selects from (bvh.cpp:132-176).
+// Any hit (ANY=true): shadow query, true iff such a triangle exists.
+// The stack lives in LDS: sc/st point at this lane's column, stride = lanes per block.
+// One call site serves both queries (ANY is a runtime flag) so that lanes tracing extension
+// rays and lanes tracing shadow rays share the same traversal loop without divergence.
+template <bool COUNT>
+ND bool traverse(const DScene& S, const Ray& r, float tmax, bool ANY, float& bestT, uint32_t& bestG, int* sc,
+                 float* st, int stride, TraceCounters& cnt) {
+    bestT = tmax;
+    bestG = NO_HIT;
+    if (!S.geometry_visible) return false;
+    // Box tests need not be exact (boxes are padded on the host), so use fast reciprocals.
+    const f3 inv = F3(__builtin_amdgcn_rcpf(r.d.x), __builtin_amdgcn_rcpf(r.d.y), __builtin_amdgcn_rcpf(r.d.z));
+    const f3 oi = F3(-r.o.x * inv.x, -r.o.y * inv.y, -r.o.z * inv.z);
+    int sp = 0;
+    int code = S.root;
+    for (;;) {
+        if (code >= 0) {
+            if (COUNT) cnt.nodes++;
+            const float4* np = reinterpret_cast<const float4*>(S.nodes + code);
+            float4 a = np[0], b = np[1], c = np[2];
+            int4 k = reinterpret_cast<const int4*>(np)[3];
+            // child 0: lo (a.x a.y a.z) hi (a.w b.x b.y); child 1: lo (b.z b.w c.x) hi (c.y c.z c.w)
+            float tx0 = fmaf(a.x, inv.x, oi.x), tx1 = fmaf(a.w, inv.x, oi.x);
+            float ty0 = fmaf(a.y, inv.y, oi.y), ty1 = fmaf(b.x, inv.y, oi.y);
+            float tz0 = fmaf(a.z, inv.z, oi.z), tz1 = fmaf(b.y, inv.z, oi.z);
+            float n0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+            float f0 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+            float ux0 = fmaf(b.z, inv.x, oi.x), ux1 = fmaf(c.y, inv.x, oi.x);
+            float uy0 = fmaf(b.w, inv.y, oi.y), uy1 = fmaf(c.z, inv.y, oi.y);
+            float uz0 = fmaf(c.x, inv.z, oi.z), uz1 = fmaf(c.w, inv.z, oi.z);
+            float n1 = fmaxf(fmaxf(fminf(ux0, ux1), fminf(uy0, uy1)), fminf(uz0, uz1));
+            float f1 = fminf(fminf(fmaxf(ux0, ux1), fmaxf(uy0, uy1)), fmaxf(uz0, uz1));
+            bool h0 = (n0 <= f0) && (f0 >= 0.f) && (n0 <= bestT);
+            bool h1 = (n1 <= f1) && (f1 >= 0.f) && (n1 <= bestT);
+            if (h0 && h1) {
+                bool swap = n1 < n0;
+                int near = swap ? k.y : k.x, far = swap ? k.x : k.y;
+                float tfar = swap ? n0 : n1;
+                sc[sp * stride] = far;
+                st[sp * stride] = tfar;
+                ++sp;
+                code = near;
+                continue;
+            }
+            if (h0) { code = k.x; continue; }
+            if (h1) { code = k.y; continue; }
+        } else {
+            uint32_t lc = ~(uint32_t)code;
+            uint32_t first = lc >> 5, count = (lc & 31u) + 1u;
+            for (uint32_t i = 0; i < count; ++i) {
+                if (COUNT) cnt.tris++;
+                const float4* tp = S.tri_isect + 4 * (first + i);
+                float4 b = tp[1], c = tp[2], dd = tp[3];
+                float e0, e1, e2;
+                edge_functions(r, F3(b.x, b.y, b.z), F3(b.w, c.x, c.y), F3(c.z, c.w, dd.x), e0, e1, e2);
+                if (!edges_accept(e0, e1, e2)) continue;
+                float4 a = tp[0];
+                f3 n = F3(a.x, a.y, a.z);
+                float t = (a.w - dot(r.o, n)) / dot(r.d, n);
+                if (!(t > 0.f) || !(t < tmax)) continue;  // geometry.cpp:37-39 with tMin = 0
+                uint32_t g = __float_as_uint(dd.y);
+                if (ANY) {
+                    bestT = t;
+                    bestG = g;
+                    return true;
+                }
+                if (t < bestT || (t == bestT && g < bestG)) {
+                    bestT = t;
+                    bestG = g;
+                }
+            }
+        }
+        // pop the next subtree that can still contain a closer hit
+        bool found = false;
+        while (sp > 0) {
+            --sp;
+            float tn = st[sp * stride];
+            if (tn <= bestT) {
+                code = sc[sp * stride];
+                found = true;
+                break;
+            }
+        }
+        if (!found) break;
+    }
+    return bestG != NO_HIT;
+}
+
+// ---------------------------------------------------------------- Intersection
+struct Isect {
+    f3 p, gn, sn, dpds, dpdt;
+    f2 st;
+    uint32_t meshID, priority, mat;
+};
+ND f3 load3(const float* a) { return F3(a[0], a[1], a[2]); }
+
+// Attributes of the winning triangle (geometry.cpp:84-112) + Chunk::Intersect ids (bvh.cpp:72-75)
+ND void fill_isect(const DScene& S, const Ray& r, uint32_t g, Isect& is) {
+    const nart_triangle& T = S.tris[g];
+    f3 v0 = load3(T.v0), v1 = load3(T.v1), v2 = load3(T.v2);
+    f3 n = cross(sub(v1, v0), sub(v2, v0));
+    float e0, e1, e2;
+    edge_functions(r, v0, v1, v2, e0, e1, e2);
+    float invDet = 1.f / (e0 + e1 + e2);
+    is.p = muls(add(add(muls(v0, e0), muls(v1, e1)), muls(v2, e2)), invDet);
+    float u = e0 * invDet;
+    float v = e1 * invDet;
+    is.gn = normalize(n);
+    float w = 1 - u - v;
+    is.sn = add(add(muls(load3(T.n0), u), muls(load3(T.n1), v)), muls(load3(T.n2), w));
+    is.st = F2((T.uv0[0] * u + T.uv1[0] * v) + T.uv2[0] * w, (T.uv0[1] * u + T.uv1[1] * v) + T.uv2[1] * w);
+    float UVDet = ((T.uv0[0] - T.uv2[0]) * (T.uv1[1] - T.uv2[1])) - ((T.uv0[1] - T.uv2[1]) * (T.uv1[0] - T.uv2[0]));
+    float invUVDet = 1.f / UVDet;
+    is.dpds = muls(add(muls(sub(v0, v2), T.uv1[1] - T.uv2[1]), muls(sub(v1, v2), T.uv2[1] - T.uv0[1])), invUVDet);
+    is.dpdt = muls(add(muls(sub(v0, v2), T.uv2[0] - T.uv1[0]), muls(sub(v1, v2), T.uv0[0] - T.uv2[0])), invUVDet);
+    uint32_t mesh = S.tri_mesh[g];
+    is.meshID = mesh;
+    is.priority = S.meshes[mesh].priority;
+    is.mat = S.meshes[mesh].material;
+}
+
+// ---------------------------------------------------------------- patterns
+ND float half_to_float(uint16_t h) {  // Imath half -> float (exact)
+    uint32_t hexpmant = ((uint32_t)h << 17) >> 4;
+    uint32_t v = ((uint32_t)h >> 15) << 31;
+    if (hexpmant >= 0x00800000u) {
+        v |= hexpmant;
+        if (hexpmant >= 0x0f800000u) v |= 0x7f800000u;
+        else v += 0x38000000u;
+    } else if (hexpmant != 0) {
+        uint32_t lc = __builtin_clz(hexpmant) - 8;
+        v |= 0x38800000u;
+        v |= (hexpmant << lc);
+        v -= (lc << 23);
+    }
+    return __uint_as_float(v);
+}
+ND f3 tex_fetch(const DScene& S, int tex, float su, float sv, int rough) {  // texturepattern.cpp:172-187
+    const DTexture& t = S.texs[tex];
+    float u = gmin(gmax(su, 0.0001f), 0.9999f);
+    float v = gmin(gmax(1.f - sv, 0.0001f), 0.9999f);
+    int iu = (int)((float)t.w * u);
+    int iv = (int)((float)t.h * v);
+    const uint16_t* px = S.tex_pool + t.offset + ((uint64_t)iv * t.w + (uint64_t)iu) * 4;
+    float rr = half_to_float(px[0]), gg = half_to_float(px[1]), bb = half_to_float(px[2]);
+    if (rough) { rr *= rr; gg *= gg; bb *= bb; }
+    return F3(rr, gg, bb);
+}
+ND f3 ptn_value(const DScene& S, const DPattern& p, f2 st) {
+    if (p.type == NART_PTN_CONSTANT) return F3(p.v[0], p.v[1], p.v[2]);
+    return tex_fetch(S, p.tex, st.x, st.y, p.rough);
+}
+
+// ---------------------------------------------------------------- BxDFs
+enum { B_LAMBERT, B_SPECULAR, B_SPECDIEL, B_DIEL, B_TS };
+struct BxDF {
+    int type;
+    uint32_t flags;  // BxDF::flags member
+    f3 rho, tau;
+    float eta, a0, ap;
+};
+
+ND float fresnel(float eta_o, float eta_i, float cosTheta) {  // bxdf.cpp:3-22
+    if (eta_o == eta_i) return 0.f;
+    float cos_o = gmin(gabs(cosTheta), 1.f);
+    float sin_o = sqrtf(1.f - (cos_o * cos_o));
+    float sin_i = (eta_o / eta_i) * sin_o;
+    if (sin_i > 1.f) return 1.f;
+    float cos_i = sqrtf(1.f - (sin_i * sin_i));
+    if (gabs(cos_o + cos_i) < 0.00001f) return 0.f;
+    float fPara = ((eta_i * cos_o) - (eta_o * cos_i)) / ((eta_i * cos_o) + (eta_o * cos_i));
+    float fPerp = ((eta_o * cos_o) - (eta_i * cos_i)) / ((eta_o * cos_o) + (eta_i * cos_i));
+    return ((fPara * fPara) + (fPerp * fPerp)) * 0.5f;
+}
+ND f3 reflect(f3 w1, f3 w2) { return sub(muls(w2, 2.f * dot(w1, w2)), w1); }  // bxdf.h:14-16
+ND float lambda_(float alpha, f3 w) {
+    float sinT = sqrtf(1.f - (w.z * w.z));
+    float tanT = (sinT / w.z);
+    return (-1.f + sqrtf(1.f + (alpha * alpha * tanT * tanT))) * 0.5f;
+}
+ND float G_(float a, f3 wo, f3 wi) { return 1.f / (1.f + lambda_(a, wo) + lambda_(a, wi)); }
+ND float G1_(float a, f3 w) { return 1.f / (1.f + lambda_(a, w)); }
+ND float D_ggx(float alpha, f3 wh) {  // torrancesparrowbrdf.cpp:19-30
+    float sinT = sqrtf(1.f - (wh.z * wh.z));
+    float tanT = (sinT / wh.z);
+    float tan2 = tanT * tanT;
+    return 1.f / ((ND_PI * alpha * alpha * ((wh.z * wh.z) * (wh.z * wh.z))) * (1.f + (tan2 / (alpha * alpha))) *
+                  (1.f + (tan2 / (alpha * alpha))));
+}
+ND float D_diel(float alpha, f3 wh) { return wh.z == 0.f ? 0.f : D_ggx(alpha, wh); }  // dielectricbrdf.cpp:19-29
+
+// VNDF sampling (dielectricbrdf.cpp:106-139 with diel=1, torrancesparrowbrdf.cpp:68-96 with diel=0)
+ND f3 sample_wh(f3 wo, float alpha, f2 sample, bool diel) {
+    f3 wo_h = normalize(F3(wo.x * alpha, wo.y * alpha, wo.z));
+    if (diel && wo.z < 0.f) wo_h = muls(wo_h, -1.f);
+    f3 T1;
+    if (diel && wo.x == 0.f && wo.y == 0.f) T1 = F3(1.f, 0.f, 0.f);
+    else T1 = F3(wo_h.y, -wo_h.x, 0.f);
+    T1 = normalize(T1);
+    f3 T2 = normalize(cross(T1, wo_h));
+    f2 vh = uniform_sample_disk(sample);
+    float s = (1.f + wo_h.z) * 0.5f;
+    vh.y = (s * vh.y) + ((1.f - s) * sqrtf(1.f - (vh.x * vh.x)));
+    f3 wh = F3(sqrtf(1.f - (vh.x * vh.x) - (vh.y * vh.y)), vh.x, vh.y);
+    wh = add(add(muls(wo_h, wh.x), muls(T1, wh.y)), muls(T2, wh.z));
+    return normalize(F3(wh.x * alpha, wh.y * alpha, wh.z));
+}
+
+ND f3 bxdf_f(const BxDF& b, f3 wo, f3 wi, bool uap, float eta_outer) {
+    if (b.type == B_LAMBERT) return muls(b.rho, ND_ONE_OVER_PI);  // lambertbrdf.cpp:7-11
+    if (b.type == B_DIEL) {                                       // dielectricbrdf.cpp:31-80
+        float alpha = uap ? b.ap : b.a0;
+        float eta_o = eta_outer, eta_i = b.eta;
+        if (wo.z < 0.f) { float t = eta_o; eta_o = eta_i; eta_i = t; }
+        if (wo.z * wi.z >= 0.f) {
+            f3 wh = normalize(add(wo, wi));
+            if (wh.z < 0.f) wh = muls(wh, -1.f);
+            float g = G_(alpha, wo, wi);
+            float d = D_diel(alpha, wh);
+            float Fr = fresnel(eta_o, eta_i, gabs(dot(wh, wo)));
+            if (wo.z * wi.z == 0.f) return F3(0.f, 0.f, 0.f);
+            return divs(muls(muls(muls(b.rho, g), d), Fr), (4.f * wo.z * wi.z));
+        }
+        f3 wh = normalize(add(muls(wo, eta_o), muls(wi, eta_i)));
+        if (wh.z < 0.f) wh = muls(wh, -1.f);
+        float Fr = fresnel(eta_o, eta_i, gabs(dot(wh, wo)));
+        if (Fr >= 1.f) return F3(0.f, 0.f, 0.f);
+        float g = G_(alpha, wo, wi);
+        float d = D_diel(alpha, wh);
+        float wiDotWh = dot(wi, wh);
+        float woDotWh = dot(wo, wh);
+        float num = g * d * (1.f - Fr) * gabs(wiDotWh) * gabs(woDotWh) * eta_o * eta_o;
+        float x = ((eta_i * wiDotWh) + (eta_o * woDotWh));
+        float denom = x * x * gabs(wo.z * wi.z);
+        float q = num / denom;
+        return mul(F3(q, q, q), b.tau);
+    }
+    if (b.type == B_TS) {  // torrancesparrowbrdf.cpp:32-51
+        float alpha = uap ? b.ap : b.a0;
+        if (wo.z < 0.f || wi.z < 0.f) return F3(0.f, 0.f, 0.f);
+        f3 wh = normalize(add(wo, wi));
+        float g = G_(alpha, wo, wi);
+        float d = D_ggx(alpha, wh);
+        float fr = fresnel(eta_outer, b.eta, dot(wh, wi));
+        if (wo.z * wi.z == 0.f) return F3(0.f, 0.f, 0.f);
+        return divs(muls(muls(muls(b.rho, g), d), fr), (4.f * wo.z * wi.z));
+    }
+    return F3(0.f, 0.f, 0.f);  // delta lobes: f == 0
+}
+
+ND float bxdf_pdf(const BxDF& b, f3 wo, f3 wi, bool uap, float eta_outer) {
+    if (b.type == B_LAMBERT) return wi.z * ND_ONE_OVER_PI;
+    if (b.type == B_DIEL) {  // dielectricbrdf.cpp:187-225
+        float eta_o = eta_outer, eta_i = b.eta;
+        if (eta_o == eta_i) return 0.f;
+        float alpha = uap ? b.ap : b.a0;
+        if (wo.z * wi.z >= 0.f) {
+            f3 wh = normalize(add(wo, wi));
+            if (wh.z < 0.f) wh = muls(wh, -1.f);
+            float cosThetaH = gabs(gmin(dot(wo, wh), 1.f));
+            float pdf = (D_diel(alpha, wh) * gmin(dot(wo, wh), 1.f) * G1_(alpha, wo)) / wo.z;
+            return gmax(0.f, pdf / (4.f * cosThetaH));
+        }
+        if (wo.z < 0.f) { float t = eta_o; eta_o = eta_i; eta_i = t; }
+        f3 wh = normalize(add(muls(wo, eta_o), muls(wi, eta_i)));
+        if (wh.z < 0.f) wh = muls(wh, -1.f);
+        float pdf = (D_diel(alpha, wh) * gmin(gabs(dot(wo, wh)), 1.f) * G1_(alpha, wo)) / gabs(wo.z);
+        float dotWiWh = dot(wi, wh);
+        float dotWoWh = dot(wo, wh);
+        float denom = (eta_i * dotWiWh + eta_o * dotWoWh);
+        float JDet = (fabsf(dotWiWh) * eta_i * eta_i) / (denom * denom);
+        return pdf * JDet;
+    }
+    if (b.type == B_TS) {  // torrancesparrowbrdf.cpp:109-124
+        float alpha = uap ? b.ap : b.a0;
+        f3 wh = normalize(add(wo, wi));
+        if (wh.z < 0.f) return 0.f;
+        float cosThetaH = gmin(dot(wo, wh), 1.f);
+        float pdf = (D_ggx(alpha, wh) * gmin(dot(wo, wh), 1.f) * G1_(alpha, wo)) / wo.z;
+        return gmax(0.f, pdf / (4.f * cosThetaH));
+    }
+    return 0.f;
+}
+ND float bxdf_eta(const BxDF& b) { return b.type == B_LAMBERT ? 0.f : b.eta; }
+
+ND f3 bxdf_sample_f(const BxDF& b, f3 wo, f3& wi, float s1, f2 sample, float& pdf, uint32_t& flags, float* alpha_i,
+                    bool uap, float eta_outer) {
+    if (b.type == B_LAMBERT) {  // lambertbrdf.cpp:13-22
+        if (alpha_i) *alpha_i = 1.f;
+        flags = F_DIFFUSE;
+        wi = cosine_sample_hemisphere(sample, pdf);
+        return bxdf_f(b, wo, wi, uap, eta_outer);
+    }
+    if (b.type == B_SPECULAR) {  // specularbrdf.cpp:14-36
+        if (alpha_i) *alpha_i = 0.f;
+        flags = F_SPECULAR;
+        wi = F3(-wo.x, -wo.y, wo.z);
+        pdf = 1.f;
+        if (wi.z == 0.f) return F3(1.f, 1.f, 1.f);
+        return divs(muls(b.rho, fresnel(eta_outer, b.eta, wi.z)), gabs(wi.z));
+    }
+    if (b.type == B_SPECDIEL) {  // speculardielectricbrdf.cpp:15-89
+        float eta_o = eta_outer, eta_i = b.eta;
+        if (eta_o == eta_i) {
+            wi = neg(wo);
+            pdf = 0.f;
+            flags |= F_TRANSMISSIVE;
+            return b.tau;
+        }
+        if (alpha_i) *alpha_i = 0.f;
+        flags = F_SPECULAR;
+        if (wo.z < 0.f) { float t = eta_o; eta_o = eta_i; eta_i = t; }
+        float Fr = fresnel(eta_o, eta_i, gabs(wo.z));
+        if (sample.x < Fr) {
+            pdf = Fr;
+            wi = F3(-wo.x, -wo.y, wo.z);
+            if (wi.z == 0.f) return F3(1.f, 1.f, 1.f);
+            float q = Fr / gabs(wi.z);
+            return mul(F3(q, q, q), b.rho);
+        }
+        pdf = 1.f - Fr;
+        float sinT_o = sqrtf(1.f - (wo.z * wo.z));
+        float sinT_i = ((eta_o / eta_i) * sinT_o);
+        if (sinT_i >= 1.f) {
+            wi = F3(-wo.x, -wo.y, wo.z);
+            return mul(F3(1.f, 1.f, 1.f), b.rho);
+        }
+        flags |= F_TRANSMISSIVE;
+        const f3 n = F3(0.f, 0.f, 1.f);
+        f3 bb = muls(n, wo.z);
+        f3 a = sub(wo, bb);
+        f3 c = muls(neg(a), (eta_o / eta_i));
+        f3 d = muls(neg(n), sqrtf(1.f - (sinT_i * sinT_i)));
+        if (wo.z < 0.f) d = muls(d, -1.f);
+        wi = normalize(add(c, d));
+        float q = ((eta_o / eta_i) * (eta_o / eta_i) * (1.f - Fr)) / gabs(wi.z);
+        return mul(F3(q, q, q), b.tau);
+    }
+    if (b.type == B_DIEL) {  // dielectricbrdf.cpp:82-183
+        float eta_o = eta_outer, eta_i = b.eta;
+        if (eta_o == eta_i) {
+            wi = neg(wo);
+            pdf = 0.f;
+            flags |= F_TRANSMISSIVE;
+            return b.tau;
+        }
+        float alpha = uap ? b.ap : b.a0;
+        if (alpha_i) *alpha_i = alpha;
+        flags = F_SPECULAR;
+        if (alpha > 0.0001f) flags = F_GLOSSY;
+        if (alpha >= 1.0f) flags = F_DIFFUSE;
+        f3 wh = sample_wh(wo, alpha, sample, true);
+        if (wo.z < 0.f) { float t = eta_o; eta_o = eta_i; eta_i = t; }
+        float Fr = fresnel(eta_o, eta_i, gabs(dot(wh, wo)));
+        if (s1 < Fr) {
+            wi = normalize(reflect(wo, wh));
+            pdf = bxdf_pdf(b, wo, wi, uap, eta_outer) * Fr;
+            return bxdf_f(b, wo, wi, uap, eta_outer);
+        }
+        float cos_o = gmin(1.f, gmax(-1.f, dot(wo, wh)));
+        float sin_o = sqrtf(1.f - (cos_o * cos_o));
+        float sin_i = ((eta_o / eta_i) * sin_o);
+        if (sin_i >= 1.f) {
+            wi = normalize(reflect(wo, wh));
+            pdf = bxdf_pdf(b, wo, wi, uap, eta_outer) * (1.f - Fr);
+            return bxdf_f(b, wo, wi, uap, eta_outer);
+        }
+        flags |= F_TRANSMISSIVE;
+        f3 bb = muls(wh, cos_o);
+        f3 a = sub(wo, bb);
+        f3 c = muls(neg(a), (eta_o / eta_i));
+        f3 d = muls(neg(wh), sqrtf(1.f - (sin_i * sin_i)));
+        if (dot(wo, wh) < 0.f) d = muls(d, -1.f);
+        wi = normalize(add(c, d));
+        pdf = bxdf_pdf(b, wo, wi, uap, eta_outer) * (1.f - Fr);
+        return bxdf_f(b, wo, wi, uap, eta_outer);
+    }
+    // B_TS: torrancesparrowbrdf.cpp:53-105
+    float alpha = uap ? b.ap : b.a0;
+    if (alpha_i) *alpha_i = alpha;
+    flags = F_SPECULAR;
+    if (alpha > 0.001f) flags = F_GLOSSY;
+    if (alpha >= 1.0f) flags = F_DIFFUSE;
+    f3 wh = sample_wh(wo, alpha, sample, false);
+    wi = normalize(reflect(wo, wh));
+    pdf = bxdf_pdf(b, wo, wi, uap, eta_outer);
+    return bxdf_f(b, wo, wi, uap, eta_outer);
+}
+
+// ---------------------------------------------------------------- BSDF (bxdf.cpp:24-115)
+struct BSDF {
+    f3 n_t, n_b, n;
+    uint32_t num;
+    BxDF b[2];
+};
+ND f3 to_local(const BSDF& s, f3 v) { return normalize(F3(dot(v, s.n_t), dot(v, s.n_b), dot(v, s.n))); }
+ND f3 to_world(const BSDF& s, f3 v) { return normalize(add(add(muls(s.n_t, v.x), muls(s.n_b, v.y)), muls(s.n, v.z))); }
+ND void build_coord_sys(BSDF& s, const Isect& is, const f3* nn) {
+    s.n_t = normalize(sub(is.dpds, muls(s.n, dot(is.dpds, s.n))));
+    s.n_b = normalize(cross(is.sn, s.n_t));
+    if (nn) {
+        s.n = normalize(to_world(s, *nn));
+        s.n_t = normalize(sub(is.dpds, muls(s.n, dot(is.dpds, s.n))));
+        s.n_b = normalize(cross(is.sn, s.n_t));
+    }
+}
+ND f3 bsdf_f(const BSDF& s, f3 wo, f3 wi, bool uap, float eta_outer) {
+    f3 f = F3(0.f, 0.f, 0.f);
+    f = add(f, bxdf_f(s.b[0], wo, wi, uap, eta_outer));
+    if (s.num > 1) f = add(f, bxdf_f(s.b[1], wo, wi, uap, eta_outer));
+    return f;
+}
+ND float bsdf_pdf(const BSDF& s, f3 wo, f3 wi, bool uap, float eta_outer) {
+    float pdf = 0.f;
+    pdf += bxdf_pdf(s.b[0], wo, wi, uap, eta_outer);
+    if (s.num > 1) pdf += bxdf_pdf(s.b[1], wo, wi, uap, eta_outer);
+    return pdf / (float)s.num;
+}
+ND f3 bsdf_sample_f(const BSDF& s, f3 wo, f3& wi, float s1, f2 sample, float& pdf, uint32_t& flags, bool uap,
+                    float eta_outer, float* alpha_i, float* eta_i) {
+    uint32_t idx = f2u8(s1 * (float)s.num);
+    s1 = gfract(s1 * (float)s.num);
+    const BxDF& sel = s.b[idx ? 1 : 0];
+    f3 f = bxdf_sample_f(sel, wo, wi, s1, sample, pdf, flags, alpha_i, uap, eta_outer);
+    if (eta_i && (flags & F_TRANSMISSIVE)) *eta_i = bxdf_eta(sel);
+    if (!(flags & F_SPECULAR)) {
+        if (s.num > 1) {
+            const BxDF& o = s.b[idx ? 0 : 1];
+            if (!(o.flags & F_SPECULAR)) {
+                float bp = bxdf_pdf(o, wo, wi, uap, eta_outer);
+                if (bp > 0.f) {
+                    pdf += bxdf_pdf(o, wo, wi, uap, eta_outer);
+                    f = add(f, bxdf_f(o, wo, wi, uap, eta_outer));
+                }
+            }
+        }
+        pdf /= (float)s.num;
+    }
+    return f;
+}
+ND float bsdf_sample_eta(const BSDF& s, float s1) { return bxdf_eta(s.b[f2u8(s1 * (float)s.num) ? 1 : 0]); }
+
+// Material::CreateBSDF (src/materials/*.cpp)
+ND void create_bsdf(const DScene& S, const Isect& is, float alphaTweak, BSDF& bs) {
+    const DMaterial& m = S.mats[is.mat];
+    bs.n = is.sn;
+    bs.num = m.type == NART_MAT_PLASTIC ? 2u : 1u;
+    if (m.has_normal) {
+        f3 n = ptn_value(S, m.normal, is.st);
+        n = muls(n, 2.f);
+        n = sub(n, F3(1.f, 1.f, 1.f));
+        build_coord_sys(bs, is, &n);
+    } else {
+        build_coord_sys(bs, is, nullptr);
+    }
+    BxDF& b0 = bs.b[0];
+    b0.tau = F3(0.f, 0.f, 0.f);
+    b0.eta = 0.f;
+    b0.a0 = 0.f;
+    b0.ap = 0.f;
+    switch (m.type) {
+        case NART_MAT_LAMBERT:  // diffusematerial.cpp:6-27
+            b0.type = B_LAMBERT;
+            b0.flags = F_DIFFUSE;
+            b0.rho = ptn_value(S, m.rho_d, is.st);
+            break;
+        case NART_MAT_SPECULAR: {  // specularmaterial.cpp:9-43
+            float alpha = 0.f;
+            float ap = 1.f - ((1.f - alpha) * alphaTweak);
+            b0.rho = ptn_value(S, m.rho_s, is.st);
+            b0.eta = ptn_value(S, m.eta, is.st).x;
+            if (ap > 0.0001f) { b0.type = B_TS; b0.flags = F_GLOSSY; b0.a0 = gmax(0.0001f, alpha); b0.ap = ap; }
+            else { b0.type = B_SPECULAR; b0.flags = F_SPECULAR; }
+            break;
+        }
+        case NART_MAT_GLASS: {  // glassmaterial.cpp:11-47
+            float alpha = ptn_value(S, m.alpha, is.st).x;
+            float ap = 1.f - ((1.f - ptn_value(S, m.alpha, is.st).x) * alphaTweak);
+            b0.rho = ptn_value(S, m.rho_s, is.st);
+            b0.tau = ptn_value(S, m.tau, is.st);
+            b0.eta = ptn_value(S, m.eta, is.st).x;
+            if (ap > 0.0001f) { b0.type = B_DIEL; b0.flags = F_GLOSSY; b0.a0 = gmax(0.0001f, alpha); b0.ap = ap; }
+            else { b0.type = B_SPECDIEL; b0.flags = F_SPECULAR; }
+            break;
+        }
+        case NART_MAT_GLOSSY: {  // glossydielectricmaterial.cpp:12-47
+            float alpha = ptn_value(S, m.alpha, is.st).x;
+            float ap = 1.f - ((1.f - alpha) * alphaTweak);
+            b0.rho = ptn_value(S, m.rho_s, is.st);
+            b0.eta = ptn_value(S, m.eta, is.st).x;
+            if (ap > 0.0001f) { b0.type = B_TS; b0.flags = F_GLOSSY; b0.a0 = gmax(0.0001f, alpha); b0.ap = ap; }
+            else { b0.type = B_SPECULAR; b0.flags = F_SPECULAR; }
+            break;
+        }
+        default: {  // NART_MAT_PLASTIC: plasticmaterial.cpp:12-51
+            float alpha = ptn_value(S, m.alpha, is.st).x;
+            float ap = 1.f - ((1.f - alpha) * alphaTweak);
+            f3 rho_d = ptn_value(S, m.rho_d, is.st);
+            f3 rho_s = ptn_value(S, m.rho_s, is.st);
+            float eta = ptn_value(S, m.eta, is.st).x;
+            b0.type = B_LAMBERT;
+            b0.flags = F_DIFFUSE;
+            b0.rho = rho_d;
+            BxDF& b1 = bs.b[1];
+            b1.rho = rho_s;
+            b1.tau = F3(0.f, 0.f, 0.f);
+            b1.eta = eta;
+            if (ap > 0.001f) { b1.type = B_TS; b1.flags = F_GLOSSY; b1.a0 = gmax(0.0001f, alpha); b1.ap = ap; }
+            else { b1.type = B_SPECULAR; b1.flags = F_SPECULAR; b1.a0 = 0.f; b1.ap = 0.f; }
+            break;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- lights
+ND uint32_t binary_search(float value, const float* v, uint32_t start, uint32_t end) {  // util.cpp:4-20
+    uint32_t i = start;
+    while (start < end) {
+        i = start + ((end - start) / 2);
+        if (v[i] > value) {
+            end = i;
+            i -= 1;
+        } else {
+            start = i + 1;
+        }
+    }
+    return i;
+}
+ND float env_pdf(const DEnvDist& d, f2 s) {  // texturepattern.cpp:104-109
+    uint32_t u = f2u32(s.x * (float)d.w);
+    uint32_t v = f2u32(s.y * (float)d.h);
+    return d.mpdf[v] * d.cpdf[v * d.w + u];
+}
+ND f2 env_sample(const DEnvDist& d, f2 s, float& pdf) {  // texturepattern.cpp:72-102
+    uint32_t lb = binary_search(s.y, d.mcdf, 0, d.h);
+    float uc = 0.f;
+    float vc = ((s.y - d.mcdf[lb]) / d.mpdf[lb]) + ((float)lb * d.invH);
+    vc = gmin(vc, 0.9999999f);
+    uint32_t v = f2u32(vc * (float)d.h);
+    if (d.mpdf[v] > 0.f) {
+        lb = binary_search(s.x, d.ccdf, v * (d.w + 1), v * (d.w + 1) + d.w);
+        lb %= (d.w + 1);
+        uc = ((s.x - d.ccdf[v * (d.w + 1) + lb]) / d.cpdf[v * d.w + lb]) + ((float)lb * d.invW);
+        uc = gmin(uc, 0.9999999f);
+        uint32_t u = f2u32(uc * (float)d.w);
+        pdf = d.mpdf[v] * d.cpdf[v * d.w + u];
+    }
+    return F2(uc, vc);
+}
+
+// Disk / ring Pdf (disklight.cpp:62-104, ringlight.cpp:170-216); sets st and tMax on a hit.
+ND float area_pdf(const DLight& L, f3 p, f3 wi, f2& st, float& tMax) {
+    f3 n = load3(L.n);
+    if (dot(wi, n) >= 0.f) return 0.f;
+    float t = (L.D - dot(p, n)) / dot(wi, n);
+    if (t < 0.f) return 0.f;
+    f3 pHit = add(p, muls(wi, t));
+    f3 c2p = sub(pHit, load3(L.center));
+    f4 c4 = F4(c2p.x, c2p.y, c2p.z, 0.f);
+    float u = dot4(c4, F4(L.axu[0], L.axu[1], L.axu[2], L.axu[3])) / L.radius;
+    float v = dot4(c4, F4(L.axv[0], L.axv[1], L.axv[2], L.axv[3])) / L.radius;
+    u = (u + 1.f) * 0.5f;
+    v = (v + 1.f) * 0.5f;
+    st = F2(u, 1.f - v);
+    float dist = c2p.x * c2p.x + c2p.y * c2p.y + c2p.z * c2p.z;
+    if (dist > L.r2) return 0.f;
+    if (L.type == NART_LIGHT_RING && dist < L.ri2) return 0.f;
+    float pdf = L.pdf_area;
+    pdf = pdf * ((t * t) / dot(neg(wi), n));
+    tMax = t;
+    return pdf;
+}
+}  // namespace nd
+
+#include "envlight.h"

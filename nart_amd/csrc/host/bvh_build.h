@@ -1,0 +1,33 @@
+// Host-side acceleration structure build for the nart render path.
+#pragma once
+
+#include <stdint.h>
+
+#include <vector>
+
+#include "../../../include/nart_scene.h"
+#include "../device/dscene.h"
+
+namespace nart {
+
+struct BuiltBVH {
+    std::vector<nd::BVHNode> nodes;   // depth-first, root = nodes[0] unless root_code < 0
+    std::vector<float> tri_isect;      // 16 floats per triangle, leaf order
+    int32_t root_code = 0;
+    uint32_t max_stack = 1;            // deepest chain of inner nodes (traversal stack bound)
+    uint32_t num_leaf_tris = 0;
+    float pad = 0.f;                   // box padding applied (world units)
+};
+
+// Which triangles the reference's octree can ever return (bvh.cpp:252-326): all of them
+// unless the root stayed a leaf (single chunk, bvh.cpp:131 -> nothing is hit) or a leaf
+// holding several chunks split and dropped all but one (bvh.cpp:187-190).
+// Returns the number of visible triangles; mask[g] = 1 for visible ones.
+uint32_t reference_visibility(const nart_scene_blob& blob, std::vector<uint8_t>& mask, bool& root_is_leaf,
+                              uint32_t& n_chunks);
+
+// Binned-SAH BVH2 over the visible triangles.  Child boxes are padded by `pad` (world units)
+// so the device's fast slab test is conservative w.r.t. the exact triangle test.
+void build_bvh(const nart_scene_blob& blob, const std::vector<uint8_t>& mask, float pad, BuiltBVH& out);
+
+}  // namespace nart

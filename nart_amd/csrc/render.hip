@@ -1,0 +1,564 @@
+// C-ABI of the MI355X render path (include/nart_hip.h): context creation (scene upload, BVH
+// build, light precomputation) and the Render()-equivalent launch sequence.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/nart_hip.h"
+#include "device/kernels.h"
+#include "host/bvh_build.h"
+
+using namespace nd;
+
+struct nart_ctx {
+    int device = 0;
+    std::string err;
+    DScene scene;
+    uint32_t stack_depth = 1;
+    int variant = 0;
+    bool counters = false;
+    // scene buffers
+    void* d_nodes = nullptr;
+    void* d_tri_isect = nullptr;
+    void* d_tris = nullptr;
+    void* d_tri_mesh = nullptr;
+    void* d_meshes = nullptr;
+    void* d_mats = nullptr;
+    void* d_lights = nullptr;
+    void* d_texs = nullptr;
+    void* d_tex_pool = nullptr;
+    // work buffers
+    size_t cap_slot_bytes = 0, cap_misc = 0;
+    uint32_t* d_slot_xy = nullptr;
+    uint32_t* d_rng = nullptr;
+    float2* d_samples = nullptr;
+    float4* d_L = nullptr;
+    uint32_t* d_bucket_ids = nullptr;
+    uint32_t* d_bucket_base = nullptr;
+    float* d_table = nullptr;
+    unsigned long long* d_counters = nullptr;
+    size_t cap_slots = 0, cap_samples = 0, cap_buckets = 0;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    bool events = false;
+    uint64_t stat_counts[5] = {0, 0, 0, 0, 0};
+};
+
+namespace {
+
+int fail(nart_ctx* c, int code, const std::string& m) {
+    if (c) c->err = m;
+    return code;
+}
+#define HIPCHK(call)                                                                             \
+    do {                                                                                         \
+        hipError_t e_ = (call);                                                                  \
+        if (e_ != hipSuccess) return fail(ctx, NART_E_HIP, std::string(#call ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+template <typename T>
+int upload(nart_ctx* ctx, void*& dst, const T* src, size_t count) {
+    size_t bytes = sizeof(T) * (count ? count : 1);
+    HIPCHK(hipMalloc(&dst, bytes));
+    if (count) HIPCHK(hipMemcpy(dst, src, sizeof(T) * count, hipMemcpyHostToDevice));
+    return NART_OK;
+}
+
+DPattern dpat(const nart_pattern& p) {
+    DPattern d;
+    d.type = p.type;
+    d.tex = p.texture;
+    d.rough = p.is_roughness;
+    d.v[0] = p.value[0];
+    d.v[1] = p.value[1];
+    d.v[2] = p.value[2];
+    return d;
+}
+
+// Per-call light constants of disklight.cpp / ringlight.cpp, computed with the same float
+// operations the reference executes on every call (vec4 * mat4 row-vector products).
+DLight dlight(const nart_light& L) {
+    DLight d;
+    std::memset(&d, 0, sizeof(d));
+    d.type = L.type;
+    d.radius = L.radius;
+    d.inner = L.inner_radius;
+    d.intensity = L.intensity;
+    d.Le = dpat(L.Le);
+    std::memcpy(d.m, L.m, sizeof(d.m));
+    f4 c = vec_mul_mat(F4(0.f, 0.f, 0.f, 1.f), L.m);
+    f4 n = vec_mul_mat(F4(0.f, 0.f, -1.f, 0.f), L.m);
+    f4 u = vec_mul_mat(F4(1.f, 0.f, 0.f, 0.f), L.m);
+    f4 v = vec_mul_mat(F4(0.f, 1.f, 0.f, 0.f), L.m);
+    d.center[0] = c.x; d.center[1] = c.y; d.center[2] = c.z;
+    d.n[0] = n.x; d.n[1] = n.y; d.n[2] = n.z;
+    d.D = dot(F3(c.x, c.y, c.z), F3(n.x, n.y, n.z));
+    d.axu[0] = u.x; d.axu[1] = u.y; d.axu[2] = u.z; d.axu[3] = u.w;
+    d.axv[0] = v.x; d.axv[1] = v.y; d.axv[2] = v.z; d.axv[3] = v.w;
+    const float pi = ND_PI;
+    if (L.type == NART_LIGHT_RING)
+        d.pdf_area = 1.f / (pi * (1.f - ((L.inner_radius * L.inner_radius) / (L.radius * L.radius))) * L.radius * L.radius);
+    else
+        d.pdf_area = 1.f / (pi * L.radius * L.radius);
+    d.r2 = L.radius * L.radius;
+    d.ri2 = L.inner_radius * L.inner_radius;
+    d.inner_ratio = L.inner_radius / L.radius;
+    d.env = -1;
+    return d;
+}
+
+int check_params(nart_ctx* ctx, const nart_render_params* p) {
+    if (!p) return fail(ctx, NART_E_INVALID, "null params");
+    if (p->integrator != NART_INTEGRATOR_PATH)
+        return fail(ctx, NART_E_UNSUPPORTED, "volume integrator not implemented on the device yet");
+    if (!p->image_width || !p->image_height || !p->bucket_size || !p->spp)
+        return fail(ctx, NART_E_INVALID, "imageWidth, imageHeight, bucketSize and spp must be > 0");
+    if (!(p->filter_width > 0.f)) return fail(ctx, NART_E_INVALID, "filterWidth must be > 0");
+    if (p->bounces > 32) return fail(ctx, NART_E_UNSUPPORTED, "bounces > 32 not supported");
+    if (ctx->scene.num_lights == 0)
+        return fail(ctx, NART_E_INVALID, "scene has no lights (reference throws in Scene::GetLight)");
+    nart_session_geometry g;
+    nart_session_geometry_of(p, &g);
+    if (g.total_width > 65535 || g.total_height > 65535) return fail(ctx, NART_E_UNSUPPORTED, "image too large");
+    return NART_OK;
+}
+
+size_t batch_slot_limit(uint32_t spp) {
+    size_t budget = (size_t)16 << 30;
+    if (const char* e = std::getenv("NART_BATCH_BYTES")) budget = (size_t)std::strtoull(e, nullptr, 10);
+    size_t per = 8 + (size_t)spp * (sizeof(float2) + sizeof(float4));
+    size_t n = budget / per;
+    return n < 256 ? 256 : n;
+}
+
+int ensure(nart_ctx* ctx, size_t slots, uint32_t spp, size_t buckets) {
+    size_t samples = slots * spp;
+    if (slots > ctx->cap_slots) {
+        if (ctx->d_slot_xy) hipFree(ctx->d_slot_xy);
+        if (ctx->d_rng) hipFree(ctx->d_rng);
+        ctx->d_slot_xy = nullptr;
+        ctx->d_rng = nullptr;
+        HIPCHK(hipMalloc(&ctx->d_slot_xy, slots * 4));
+        HIPCHK(hipMalloc(&ctx->d_rng, slots * 4));
+        ctx->cap_slots = slots;
+    }
+    if (samples > ctx->cap_samples) {
+        if (ctx->d_samples) hipFree(ctx->d_samples);
+        if (ctx->d_L) hipFree(ctx->d_L);
+        ctx->d_samples = nullptr;
+        ctx->d_L = nullptr;
+        HIPCHK(hipMalloc(&ctx->d_samples, samples * sizeof(float2)));
+        HIPCHK(hipMalloc(&ctx->d_L, samples * sizeof(float4)));
+        ctx->cap_samples = samples;
+    }
+    if (buckets > ctx->cap_buckets) {
+        if (ctx->d_bucket_ids) hipFree(ctx->d_bucket_ids);
+        if (ctx->d_bucket_base) hipFree(ctx->d_bucket_base);
+        ctx->d_bucket_ids = ctx->d_bucket_base = nullptr;
+        HIPCHK(hipMalloc(&ctx->d_bucket_ids, buckets * 4));
+        HIPCHK(hipMalloc(&ctx->d_bucket_base, buckets * 4));
+        ctx->cap_buckets = buckets;
+    }
+    return NART_OK;
+}
+
+template <int MAXL, bool COUNT>
+void launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
+    dim3 grid((a.n_slots + 255) / 256), block(256);
+    size_t lds = (size_t)ctx->stack_depth * 256 * 8;
+    hipLaunchKernelGGL((k_render<MAXL, COUNT>), grid, block, lds, st, ctx->scene, a);
+}
+
+void dispatch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
+    const bool c = ctx->counters;
+    if (a.bounces <= 10) c ? launch_render<10, true>(ctx, a, st) : launch_render<10, false>(ctx, a, st);
+    else if (a.bounces <= 16) c ? launch_render<16, true>(ctx, a, st) : launch_render<16, false>(ctx, a, st);
+    else c ? launch_render<32, true>(ctx, a, st) : launch_render<32, false>(ctx, a, st);
+}
+
+// Render a bucket list into device tiles (list order).  Shared by all entry points.
+int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* ids, uint32_t n, float* d_tiles,
+                   hipStream_t st, nart_render_stats* stats) {
+    int rc = check_params(ctx, p);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(ctx->device));
+    nart_session_geometry g;
+    nart_session_geometry_of(p, &g);
+    const uint32_t nb_total = g.n_buckets_x * g.n_buckets_y;
+    for (uint32_t i = 0; i < n; ++i)
+        if (ids[i] >= nb_total) return fail(ctx, NART_E_INVALID, "bucket id out of range");
+    float table[64];
+    nart_filter_table(table);
+    if (!ctx->d_table) HIPCHK(hipMalloc(&ctx->d_table, 64 * sizeof(float)));
+    HIPCHK(hipMemcpyAsync(ctx->d_table, table, sizeof(table), hipMemcpyHostToDevice, st));
+    if (!ctx->d_counters) HIPCHK(hipMalloc(&ctx->d_counters, 8 * sizeof(unsigned long long)));
+    if (ctx->counters) HIPCHK(hipMemsetAsync(ctx->d_counters, 0, 8 * sizeof(unsigned long long), st));
+    if (!ctx->events) {
+        for (auto& e : ctx->ev) HIPCHK(hipEventCreate(&e));
+        ctx->events = true;
+    }
+    const size_t limit = batch_slot_limit(p->spp);
+    const uint32_t tpx = g.tile_size * g.tile_size;
+    double kernel_ms = 0.0, splat_ms = 0.0;
+    uint32_t launches = 0;
+    uint64_t traced = 0, counted = 0;
+    uint32_t b0 = 0;
+    std::vector<uint32_t> xy, base;
+    while (b0 < n) {
+        // gather a batch of buckets whose traced pixels fit the slot budget
+        xy.clear();
+        base.clear();
+        uint32_t b1 = b0;
+        while (b1 < n) {
+            uint32_t id = ids[b1];
+            uint32_t bx = id % g.n_buckets_x, by = id / g.n_buckets_x;
+            uint32_t x0 = p->bucket_size * bx, y0 = p->bucket_size * by;
+            uint32_t x1 = std::min(p->bucket_size * (bx + 1), g.total_width);   // render.cpp:163-168
+            uint32_t y1 = std::min(p->bucket_size * (by + 1), g.total_height);
+            size_t cnt = (size_t)(x1 - x0) * (y1 - y0);
+            if (b1 > b0 && xy.size() + cnt > limit) break;
+            base.push_back((uint32_t)xy.size());
+            for (uint32_t y = y0; y < y1; ++y)
+                for (uint32_t x = x0; x < x1; ++x) {
+                    xy.push_back(x | (y << 16));
+                    if (x < p->image_width && y < p->image_height) ++counted;
+                }
+            ++b1;
+        }
+        const uint32_t nslots = (uint32_t)xy.size(), nbk = b1 - b0;
+        traced += (uint64_t)nslots * p->spp;
+        rc = ensure(ctx, nslots, p->spp, nbk);
+        if (rc) return rc;
+        HIPCHK(hipMemcpyAsync(ctx->d_slot_xy, xy.data(), (size_t)nslots * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(ctx->d_bucket_ids, ids + b0, (size_t)nbk * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(ctx->d_bucket_base, base.data(), (size_t)nbk * 4, hipMemcpyHostToDevice, st));
+        RenderArgs ra;
+        ra.slot_xy = ctx->d_slot_xy;
+        ra.samples = ctx->d_samples;
+        ra.rng0 = ctx->d_rng;
+        ra.Lout = ctx->d_L;
+        ra.n_slots = nslots;
+        ra.spp = p->spp;
+        ra.bounces = p->bounces;
+        ra.W = p->image_width;
+        ra.H = p->image_height;
+        ra.totalW = g.total_width;
+        ra.stack_depth = ctx->stack_depth;
+        ra.gamma = p->roughening_factor * p->roughening_factor;
+        ra.counters = ctx->d_counters;
+        hipLaunchKernelGGL(k_latin, dim3((nslots + 255) / 256), dim3(256), 0, st, ra);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(ctx->ev[0], st));
+        dispatch_render(ctx, ra, st);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(ctx->ev[1], st));
+        SplatArgs sa;
+        sa.bucket_ids = ctx->d_bucket_ids;
+        sa.bucket_base = ctx->d_bucket_base;
+        sa.samples = ctx->d_samples;
+        sa.Lout = ctx->d_L;
+        sa.tiles = d_tiles + (size_t)b0 * tpx * 5;
+        sa.table = ctx->d_table;
+        sa.n_buckets = nbk;
+        sa.spp = p->spp;
+        sa.B = p->bucket_size;
+        sa.fb = g.filter_bounds;
+        sa.tile = g.tile_size;
+        sa.nbx = g.n_buckets_x;
+        sa.totalW = g.total_width;
+        sa.totalH = g.total_height;
+        sa.fw = p->filter_width;
+        uint64_t nthreads = (uint64_t)nbk * tpx;
+        hipLaunchKernelGGL(k_splat, dim3((uint32_t)((nthreads + 255) / 256)), dim3(256), 0, st, sa);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(ctx->ev[2], st));
+        HIPCHK(hipEventSynchronize(ctx->ev[2]));
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]));
+        kernel_ms += ms;
+        HIPCHK(hipEventElapsedTime(&ms, ctx->ev[1], ctx->ev[2]));
+        splat_ms += ms;
+        ++launches;
+        b0 = b1;
+    }
+    if (stats) {
+        stats->kernel_ms += kernel_ms;
+        stats->splat_ms += splat_ms;
+        stats->kernel_launches += launches;
+        stats->traced_samples += traced;
+        stats->samples += counted * p->spp;
+        if (ctx->counters) {
+            unsigned long long c[8];
+            HIPCHK(hipMemcpy(c, ctx->d_counters, sizeof(c), hipMemcpyDeviceToHost));
+            stats->rays_extend += c[0];
+            stats->rays_shadow += c[1];
+            stats->node_visits += c[2];
+            stats->tri_tests += c[3];
+            stats->bounces += c[4];
+        }
+    }
+    return NART_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) {
+    if (!blob || !out) return NART_E_INVALID;
+    nart_ctx* ctx = new (std::nothrow) nart_ctx();
+    if (!ctx) return NART_E_OOM;
+    *out = nullptr;
+    ctx->device = device_id;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device_id || device_id < 0) {
+        delete ctx;
+        return NART_E_HIP;
+    }
+    int rc = NART_OK;
+    auto bail = [&](int code) {
+        nart_hip_destroy(ctx);
+        return code;
+    };
+    if (hipSetDevice(device_id) != hipSuccess) return bail(NART_E_HIP);
+    for (uint32_t l = 0; l < blob->num_lights; ++l)
+        if (blob->lights[l].type == NART_LIGHT_ENVIRONMENT) {
+            ctx->err = "environment lights are not supported on the device yet";
+            return bail(NART_E_UNSUPPORTED);
+        }
+    if (blob->medium.present) return bail(NART_E_UNSUPPORTED);
+    // reference octree visibility (Q14) + device BVH
+    std::vector<uint8_t> mask;
+    bool root_leaf = false;
+    uint32_t n_chunks = 0;
+    nart::reference_visibility(*blob, mask, root_leaf, n_chunks);
+    float maxabs = 1.f;
+    for (uint32_t g = 0; g < blob->num_triangles; ++g) {
+        const nart_triangle& T = blob->triangles[g];
+        for (int k = 0; k < 3; ++k)
+            maxabs = std::max(maxabs, std::max(std::fabs(T.v0[k]), std::max(std::fabs(T.v1[k]), std::fabs(T.v2[k]))));
+    }
+    for (int k = 12; k < 15; ++k) maxabs = std::max(maxabs, std::fabs(blob->camera.m[k]));
+    for (int k = 3; k < 16; k += 4) maxabs = std::max(maxabs, std::fabs(blob->camera.m[k]));
+    nart::BuiltBVH bvh;
+    nart::build_bvh(*blob, mask, maxabs * 6.103515625e-05f + 1e-6f, bvh);
+    ctx->stack_depth = std::max<uint32_t>(bvh.max_stack + 1, 2);
+    if ((rc = upload(ctx, ctx->d_nodes, bvh.nodes.data(), bvh.nodes.size()))) return bail(rc);
+    if ((rc = upload(ctx, ctx->d_tri_isect, bvh.tri_isect.data(), bvh.tri_isect.size()))) return bail(rc);
+    if ((rc = upload(ctx, ctx->d_tris, blob->triangles, blob->num_triangles))) return bail(rc);
+    std::vector<uint32_t> tri_mesh(blob->num_triangles);
+    std::vector<DMesh> meshes(blob->num_meshes);
+    for (uint32_t m = 0; m < blob->num_meshes; ++m) {
+        meshes[m].material = blob->meshes[m].material;
+        meshes[m].priority = blob->meshes[m].priority & 0xFFu;
+        for (uint32_t i = 0; i < blob->meshes[m].num_tris; ++i) tri_mesh[blob->meshes[m].first_tri + i] = m;
+    }
+    if (blob->num_meshes >= (1u << 24)) return bail(NART_E_UNSUPPORTED);
+    if ((rc = upload(ctx, ctx->d_tri_mesh, tri_mesh.data(), tri_mesh.size()))) return bail(rc);
+    if ((rc = upload(ctx, ctx->d_meshes, meshes.data(), meshes.size()))) return bail(rc);
+    std::vector<DMaterial> mats(blob->num_materials);
+    for (uint32_t i = 0; i < blob->num_materials; ++i) {
+        const nart_material& m = blob->materials[i];
+        DMaterial& d = mats[i];
+        d.type = m.type;
+        d.has_normal = (m.type == NART_MAT_GLASS) ? 0 : m.has_normal;  // glassmaterial.cpp:3-9
+        d.rho_d = dpat(m.rho_d);
+        d.rho_s = dpat(m.rho_s);
+        d.tau = dpat(m.tau);
+        d.eta = dpat(m.eta);
+        d.alpha = dpat(m.alpha);
+        d.normal = dpat(m.normal);
+    }
+    if ((rc = upload(ctx, ctx->d_mats, mats.data(), mats.size()))) return bail(rc);
+    std::vector<DLight> lights;
+    for (uint32_t l = 0; l < blob->num_lights; ++l) lights.push_back(dlight(blob->lights[l]));
+    if ((rc = upload(ctx, ctx->d_lights, lights.data(), lights.size()))) return bail(rc);
+    std::vector<DTexture> texs(blob->num_textures);
+    size_t pool = 0;
+    for (uint32_t t = 0; t < blob->num_textures; ++t) {
+        texs[t].w = blob->textures[t].width;
+        texs[t].h = blob->textures[t].height;
+        texs[t].offset = pool;
+        pool += (size_t)texs[t].w * texs[t].h * 4;
+    }
+    std::vector<uint16_t> tex_pool(pool ? pool : 1);
+    for (uint32_t t = 0; t < blob->num_textures; ++t)
+        std::memcpy(&tex_pool[texs[t].offset], blob->textures[t].rgba, (size_t)texs[t].w * texs[t].h * 8);
+    if ((rc = upload(ctx, ctx->d_texs, texs.data(), texs.size()))) return bail(rc);
+    if ((rc = upload(ctx, ctx->d_tex_pool, tex_pool.data(), tex_pool.size()))) return bail(rc);
+
+    DScene& S = ctx->scene;
+    std::memset(&S, 0, sizeof(S));
+    S.nodes = (const BVHNode*)ctx->d_nodes;
+    S.tri_isect = (const float4*)ctx->d_tri_isect;
+    S.tris = (const nart_triangle*)ctx->d_tris;
+    S.tri_mesh = (const uint32_t*)ctx->d_tri_mesh;
+    S.meshes = (const DMesh*)ctx->d_meshes;
+    S.mats = (const DMaterial*)ctx->d_mats;
+    S.lights = (const DLight*)ctx->d_lights;
+    S.texs = (const DTexture*)ctx->d_texs;
+    S.tex_pool = (const uint16_t*)ctx->d_tex_pool;
+    S.envs = nullptr;
+    S.num_lights = blob->num_lights;
+    S.num_tris = blob->num_triangles;
+    S.root = bvh.root_code;
+    S.geometry_visible = (!root_leaf && bvh.num_leaf_tris > 0) ? 1 : 0;
+    std::memcpy(S.cam_m, blob->camera.m, sizeof(S.cam_m));
+    // glm::tan(glm::radians(fov)) with the host libm, as the reference (pinholecamera.cpp:20)
+    S.cam_tan = std::tan(blob->camera.fov * (float)0.01745329251994329576923690768489);
+    *out = ctx;
+    return NART_OK;
+}
+
+void nart_hip_destroy(nart_ctx* ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    void* bufs[] = {ctx->d_nodes, ctx->d_tri_isect, ctx->d_tris, ctx->d_tri_mesh, ctx->d_meshes, ctx->d_mats,
+                    ctx->d_lights, ctx->d_texs, ctx->d_tex_pool, ctx->d_slot_xy, ctx->d_rng, ctx->d_samples,
+                    ctx->d_L, ctx->d_bucket_ids, ctx->d_bucket_base, ctx->d_table, ctx->d_counters};
+    for (void* b : bufs)
+        if (b) hipFree(b);
+    if (ctx->events)
+        for (auto& e : ctx->ev) hipEventDestroy(e);
+    delete ctx;
+}
+
+const char* nart_hip_last_error(const nart_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int nart_hip_set_counters(nart_ctx* ctx, int enable) {
+    if (!ctx) return NART_E_INVALID;
+    ctx->counters = enable != 0;
+    return NART_OK;
+}
+
+int nart_hip_set_variant(nart_ctx* ctx, int variant) {
+    if (!ctx) return NART_E_INVALID;
+    if (variant != 0) return fail(ctx, NART_E_UNSUPPORTED, "only the megakernel variant (0) is built");
+    ctx->variant = variant;
+    return NART_OK;
+}
+
+int nart_hip_render_buckets_async(nart_ctx* ctx, const nart_render_params* p, const uint32_t* bucket_ids,
+                                  uint32_t n_buckets, nart_pixel* d_tiles, void* stream, nart_render_stats* stats) {
+    if (!ctx || !bucket_ids || !d_tiles) return NART_E_INVALID;
+    auto t0 = std::chrono::steady_clock::now();
+    int rc = render_buckets(ctx, p, bucket_ids, n_buckets, reinterpret_cast<float*>(d_tiles), (hipStream_t)stream, stats);
+    if (stats) stats->render_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
+int nart_hip_combine_async(nart_ctx* ctx, const nart_render_params* p, const nart_pixel* d_tiles, nart_pixel* d_image,
+                           void* stream) {
+    if (!ctx || !p || !d_tiles || !d_image) return NART_E_INVALID;
+    HIPCHK(hipSetDevice(ctx->device));
+    nart_session_geometry g;
+    nart_session_geometry_of(p, &g);
+    CombineArgs ca;
+    ca.tiles = reinterpret_cast<const float*>(d_tiles);
+    ca.image = reinterpret_cast<float*>(d_image);
+    ca.W = p->image_width;
+    ca.H = p->image_height;
+    ca.B = p->bucket_size;
+    ca.fb = g.filter_bounds;
+    ca.tile = g.tile_size;
+    ca.nbx = g.n_buckets_x;
+    ca.nby = g.n_buckets_y;
+    ca.totalW = g.total_width;
+    ca.totalH = g.total_height;
+    uint64_t n = (uint64_t)g.total_width * g.total_height;
+    hipLaunchKernelGGL(k_combine, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ca);
+    HIPCHK(hipGetLastError());
+    return NART_OK;
+}
+
+int nart_hip_render(nart_ctx* ctx, const nart_render_params* p, nart_pixel* image, nart_render_stats* stats) {
+    if (!ctx || !p || !image) return NART_E_INVALID;
+    auto t0 = std::chrono::steady_clock::now();
+    int rc = check_params(ctx, p);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(ctx->device));
+    nart_session_geometry g;
+    nart_session_geometry_of(p, &g);
+    const uint32_t nb = g.n_buckets_x * g.n_buckets_y;
+    std::vector<uint32_t> ids(nb);
+    for (uint32_t i = 0; i < nb; ++i) ids[i] = i;
+    size_t tile_bytes = (size_t)nb * g.tile_size * g.tile_size * sizeof(nart_pixel);
+    size_t img_bytes = (size_t)g.total_width * g.total_height * sizeof(nart_pixel);
+    void *d_tiles = nullptr, *d_img = nullptr;
+    HIPCHK(hipMalloc(&d_tiles, tile_bytes));
+    if (hipMalloc(&d_img, img_bytes) != hipSuccess) {
+        hipFree(d_tiles);
+        return fail(ctx, NART_E_OOM, "hipMalloc image");
+    }
+    rc = render_buckets(ctx, p, ids.data(), nb, (float*)d_tiles, 0, stats);
+    if (!rc) rc = nart_hip_combine_async(ctx, p, (const nart_pixel*)d_tiles, (nart_pixel*)d_img, 0);
+    if (!rc && hipMemcpy(image, d_img, img_bytes, hipMemcpyDeviceToHost) != hipSuccess)
+        rc = fail(ctx, NART_E_HIP, "copy image");
+    hipFree(d_tiles);
+    hipFree(d_img);
+    if (stats) stats->render_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
+int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t x0, uint32_t y0, uint32_t w,
+                            uint32_t h, float* out) {
+    if (!ctx || !p || !out) return NART_E_INVALID;
+    int rc = check_params(ctx, p);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(ctx->device));
+    nart_session_geometry g;
+    nart_session_geometry_of(p, &g);
+    if (x0 + w > g.total_width || y0 + h > g.total_height) return fail(ctx, NART_E_INVALID, "rect out of range");
+    std::vector<uint32_t> xy;
+    for (uint32_t y = y0; y < y0 + h; ++y)
+        for (uint32_t x = x0; x < x0 + w; ++x) xy.push_back(x | (y << 16));
+    uint32_t n = (uint32_t)xy.size();
+    rc = ensure(ctx, n, p->spp, 1);
+    if (rc) return rc;
+    HIPCHK(hipMemcpy(ctx->d_slot_xy, xy.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+    if (!ctx->d_counters) HIPCHK(hipMalloc(&ctx->d_counters, 8 * sizeof(unsigned long long)));
+    RenderArgs ra;
+    ra.slot_xy = ctx->d_slot_xy;
+    ra.samples = ctx->d_samples;
+    ra.rng0 = ctx->d_rng;
+    ra.Lout = ctx->d_L;
+    ra.n_slots = n;
+    ra.spp = p->spp;
+    ra.bounces = p->bounces;
+    ra.W = p->image_width;
+    ra.H = p->image_height;
+    ra.totalW = g.total_width;
+    ra.stack_depth = ctx->stack_depth;
+    ra.gamma = p->roughening_factor * p->roughening_factor;
+    ra.counters = ctx->d_counters;
+    hipLaunchKernelGGL(k_latin, dim3((n + 255) / 256), dim3(256), 0, 0, ra);
+    dispatch_render(ctx, ra, 0);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(out, ctx->d_L, (size_t)n * p->spp * sizeof(float4), hipMemcpyDeviceToHost));
+    return NART_OK;
+}
+
+int nart_hip_eval_sincos(nart_ctx* ctx, const float* x, uint32_t n, float* s, float* c) {
+    if (!ctx || !x || !s || !c) return NART_E_INVALID;
+    HIPCHK(hipSetDevice(ctx->device));
+    float *dx = nullptr, *ds = nullptr, *dc = nullptr;
+    HIPCHK(hipMalloc(&dx, (size_t)n * 4 + 4));
+    HIPCHK(hipMalloc(&ds, (size_t)n * 4 + 4));
+    HIPCHK(hipMalloc(&dc, (size_t)n * 4 + 4));
+    HIPCHK(hipMemcpy(dx, x, (size_t)n * 4, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_sincos, dim3((n + 255) / 256), dim3(256), 0, 0, dx, n, ds, dc);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(s, ds, (size_t)n * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(c, dc, (size_t)n * 4, hipMemcpyDeviceToHost));
+    hipFree(dx);
+    hipFree(ds);
+    hipFree(dc);
+    return NART_OK;
+}
+
+}  // extern "C"

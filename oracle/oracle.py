@@ -1,0 +1,113 @@
+"""ctypes wrapper of the CPU restatement (oracle/nart_oracle.c).  TEST INFRASTRUCTURE ONLY:
+imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, never by the
+product path.  PARITY UNPINNED (see nart_oracle.h)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "libnart_oracle.so")
+
+_lib = None
+
+
+def default_threads():
+    """One worker per host core, capped at 16 (the GPU box's CPU share per GPU)."""
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+    return LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        _lib = ctypes.CDLL(LIB)
+        P = ctypes.c_void_p
+        _lib.oracle_create.argtypes = [P, ctypes.POINTER(P)]
+        _lib.oracle_destroy.argtypes = [P]
+        _lib.oracle_render.argtypes = [P, P, P, ctypes.c_int]
+        _lib.oracle_render_buckets.argtypes = [P, P, P, ctypes.c_uint32, P, ctypes.c_int]
+        _lib.oracle_render_samples.argtypes = [P, P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                               ctypes.c_uint32, P, P]
+        _lib.oracle_bvh_stats.argtypes = [P, P, P, P, P]
+        _lib.oracle_rng_stream.argtypes = [ctypes.c_uint32, ctypes.c_uint32, P]
+        _lib.oracle_latin_square.argtypes = [ctypes.c_uint32, ctypes.c_uint32, P, P]
+        _lib.oracle_fresnel.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_float]
+        _lib.oracle_fresnel.restype = ctypes.c_float
+    return _lib
+
+
+class Oracle:
+    def __init__(self, scene):
+        self.scene = scene  # keeps the blob alive
+        self._h = ctypes.c_void_p()
+        rc = lib().oracle_create(ctypes.c_void_p(scene.blob), ctypes.byref(self._h))
+        if rc:
+            raise RuntimeError("oracle_create failed: %d" % rc)
+
+    def render(self, p, threads=None):
+        from nart_amd import session_geometry
+        g = session_geometry(p)
+        img = np.zeros((g.total_height, g.total_width, 5), np.float32)
+        rc = lib().oracle_render(self._h, ctypes.byref(p), img.ctypes.data, threads or default_threads())
+        if rc:
+            raise RuntimeError("oracle_render failed: %d" % rc)
+        return img
+
+    def render_buckets(self, p, ids, threads=None):
+        from nart_amd import session_geometry
+        g = session_geometry(p)
+        ids = np.ascontiguousarray(ids, np.uint32)
+        tiles = np.zeros((len(ids), g.tile_size * g.tile_size, 5), np.float32)
+        rc = lib().oracle_render_buckets(self._h, ctypes.byref(p), ids.ctypes.data, len(ids), tiles.ctypes.data,
+                                         threads or default_threads())
+        if rc:
+            raise RuntimeError("oracle_render_buckets failed: %d" % rc)
+        return tiles
+
+    def render_samples(self, p, x0, y0, w, h, with_uv=False):
+        out = np.zeros((h, w, p.spp, 4), np.float32)
+        uv = np.zeros((h, w, p.spp, 2), np.float32) if with_uv else None
+        rc = lib().oracle_render_samples(self._h, ctypes.byref(p), x0, y0, w, h, out.ctypes.data,
+                                         uv.ctypes.data if with_uv else None)
+        if rc:
+            raise RuntimeError("oracle_render_samples failed: %d" % rc)
+        return (out, uv) if with_uv else out
+
+    def bvh_stats(self):
+        nc, mx, rl = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        gr = (ctypes.c_uint32 * 4)()
+        lib().oracle_bvh_stats(self._h, ctypes.byref(nc), ctypes.byref(mx), ctypes.byref(rl), gr)
+        return {"chunks": nc.value, "max_chunk_tris": mx.value, "root_is_leaf": bool(rl.value),
+                "grid": tuple(gr[:3]), "reachable_tris": gr[3]}
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().oracle_destroy(self._h)
+        except Exception:
+            pass
+
+
+def rng_stream(seed, n):
+    out = np.zeros(n, np.float32)
+    lib().oracle_rng_stream(seed, n, out.ctypes.data)
+    return out
+
+
+def latin_square(seed, spp):
+    out = np.zeros((spp, 2), np.float32)
+    st = ctypes.c_uint32()
+    lib().oracle_latin_square(seed, spp, out.ctypes.data, ctypes.byref(st))
+    return out, st.value
+
+
+def fresnel(eta_o, eta_i, c):
+    return lib().oracle_fresnel(eta_o, eta_i, c)

@@ -1,0 +1,45 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (REPO, os.path.join(REPO, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box via gpurun)")
+
+
+@pytest.fixture(scope="session")
+def built():
+    from nart_amd import build as nb
+    nb.build_scene_lib()
+    import oracle
+    oracle.build()
+    return True
+
+
+@pytest.fixture(scope="session")
+def glass_scene(built, tmp_path_factory):
+    import nart_amd
+    from nart_amd import scenes
+    return nart_amd.Scene(scenes.glass_sphere(str(tmp_path_factory.mktemp("glassSphere"))))
+
+
+@pytest.fixture(scope="session")
+def cornell_scene(built, tmp_path_factory):
+    import nart_amd
+    from nart_amd import scenes
+    return nart_amd.Scene(scenes.cornell(str(tmp_path_factory.mktemp("cornell"))))
+
+
+@pytest.fixture(scope="session")
+def gpu(built):
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    from nart_amd import build as nb
+    nb.build_hip_lib()
+    return True

@@ -1,0 +1,51 @@
+"""Quick GPU timing of the render path (development aid, not the bench contract)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import nart_amd  # noqa: E402
+from nart_amd import scenes  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default="glass")
+    ap.add_argument("-w", type=int, default=1920)
+    ap.add_argument("-H", type=int, default=1080)
+    ap.add_argument("-s", type=int, default=16)
+    ap.add_argument("--counters", action="store_true")
+    ap.add_argument("--reps", type=int, default=2)
+    a = ap.parse_args()
+    path = scenes.glass_sphere() if a.scene == "glass" else scenes.cornell()
+    scene = nart_amd.Scene(path)
+    p = nart_amd.load_sessions(path)[0]
+    p.image_width, p.image_height, p.spp = a.w, a.H, a.s
+    r = nart_amd.HipRenderer(scene)
+    for rep in range(a.reps):
+        st = nart_amd.RenderStats()
+        t = time.time()
+        r.render(p, st)
+        dt = time.time() - t
+        d = st.as_dict()
+        d["wall_s"] = dt
+        d["msamples_per_s_kernel"] = d["samples"] / (d["kernel_ms"] * 1e3)
+        d["msamples_per_s_wall"] = d["samples"] / dt / 1e6
+        print(json.dumps(d), flush=True)
+    if a.counters:
+        r.set_counters(True)
+        st = nart_amd.RenderStats()
+        r.render(p, st)
+        d = st.as_dict()
+        n = d["traced_samples"]
+        d.update({k + "_per_sample": d[k] / n for k in ("rays_extend", "rays_shadow", "node_visits", "tri_tests",
+                                                          "bounces")})
+        print(json.dumps(d), flush=True)
+
+
+if __name__ == "__main__":
+    main()
