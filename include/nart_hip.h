@@ -37,6 +37,7 @@ typedef struct nart_render_stats {
     uint64_t traced_samples;/* samples actually traced (incl. extra rows, render.cpp:164) */
     /* Counter pass only (nart_hip_set_counters(ctx,1)); zero otherwise. */
     uint64_t rays_extend, rays_shadow, node_visits, tri_tests, bounces;
+    double latin_ms;        /* device time of the LatinSquare kernel                    */
 } nart_render_stats;
 
 /* Upload the scene, build the device BVH.  device_id: HIP ordinal. */

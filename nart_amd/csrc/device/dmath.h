@@ -77,17 +77,17 @@ struct SinCosT {
     double hpi_inv, hpi, c0, c1, c2, c3, c4, s1, s2, s3;
 };
 
-// __sincosf_table (glibc sysdeps/ieee754/flt-32/s_sincosf_data.c), !TOINT_INTRINSICS
-static __constant__ const SinCosT kSinCosT[2] = {
-    {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, 0x1p0, -0x1.ffffffd0c621cp-2,
-     0x1.55553e1068f19p-5, -0x1.6c087e89a359dp-10, 0x1.99343027bf8c3p-16, -0x1.555545995a603p-3,
-     0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13},
-    {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, -0x1p0, 0x1.ffffffd0c621cp-2,
-     -0x1.55553e1068f19p-5, 0x1.6c087e89a359dp-10, -0x1.99343027bf8c3p-16, -0x1.555545995a603p-3,
-     0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13}};
-ND const SinCosT* sincos_table(int k) { return &kSinCosT[k]; }
-ND uint32_t abstop12(float x) { return (__float_as_uint(x) >> 20) & 0x7ff; }
-ND float sinf_poly(double x, double x2, const SinCosT* p, int n) {
+// __sincosf_table (glibc sysdeps/ieee754/flt-32/s_sincosf_data.c), !TOINT_INTRINSICS:
+// entry 1 is entry 0 with the cosine polynomial negated (multiplying by +-1 is exact).
+NHD SinCosT sincos_table(int k) {
+    const double c = k ? -1.0 : 1.0;
+    SinCosT t = {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, c * 0x1p0,
+                 c * -0x1.ffffffd0c621cp-2, c * 0x1.55553e1068f19p-5, c * -0x1.6c087e89a359dp-10,
+                 c * 0x1.99343027bf8c3p-16, -0x1.555545995a603p-3, 0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13};
+    return t;
+}
+NHD uint32_t abstop12(float x) { return (__builtin_bit_cast(uint32_t, x) >> 20) & 0x7ff; }
+NHD float sinf_poly(double x, double x2, const SinCosT* p, int n) {
     if ((n & 1) == 0) {
         double x3 = x * x2;
         double s1 = p->s2 + x2 * p->s3;
@@ -102,7 +102,7 @@ ND float sinf_poly(double x, double x2, const SinCosT* p, int n) {
     double c = c1 + x4 * p->c2;
     return (float)(c + x6 * c2);
 }
-ND double reduce_fast(double x, const SinCosT* p, int* np) {
+NHD double reduce_fast(double x, const SinCosT* p, int* np) {
     double r = x * p->hpi_inv;
     int n = ((int32_t)r + 0x800000) >> 24;
     *np = n;
@@ -110,35 +110,35 @@ ND double reduce_fast(double x, const SinCosT* p, int* np) {
 }
 // Valid for |y| < 120 (the reference only evaluates angles in [0, 2*pi]); larger inputs
 // would need glibc's reduce_large, which the render path never reaches.
-ND float glibc_sinf(float y) {
+NHD float glibc_sinf(float y) {
     double x = y;
-    const SinCosT* p = sincos_table(0);
+    SinCosT t0 = sincos_table(0);
     const float pio4f = (float)0x1.921FB54442D18p-1;
     if (abstop12(y) < abstop12(pio4f)) {
         double s = x * x;
         if (abstop12(y) < abstop12(0x1p-12f)) return y;
-        return sinf_poly(x, s, p, 0);
+        return sinf_poly(x, s, &t0, 0);
     }
     int n;
-    x = reduce_fast(x, p, &n);
-    double s = p->sign[n & 3];
-    if (n & 2) p = sincos_table(1);
-    return sinf_poly(x * s, x * x, p, n);
+    x = reduce_fast(x, &t0, &n);
+    double s = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;  // t0.sign[n & 3]
+    SinCosT t = sincos_table((n & 2) ? 1 : 0);
+    return sinf_poly(x * s, x * x, &t, n);
 }
-ND float glibc_cosf(float y) {
+NHD float glibc_cosf(float y) {
     double x = y;
-    const SinCosT* p = sincos_table(0);
+    SinCosT t0 = sincos_table(0);
     const float pio4f = (float)0x1.921FB54442D18p-1;
     if (abstop12(y) < abstop12(pio4f)) {
         double x2 = x * x;
         if (abstop12(y) < abstop12(0x1p-12f)) return 1.0f;
-        return sinf_poly(x, x2, p, 1);
+        return sinf_poly(x, x2, &t0, 1);
     }
     int n;
-    x = reduce_fast(x, p, &n);
-    double s = p->sign[n & 3];
-    if (n & 2) p = sincos_table(1);
-    return sinf_poly(x * s, x * x, p, n ^ 1);
+    x = reduce_fast(x, &t0, &n);
+    double s = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;  // t0.sign[n & 3]
+    SinCosT t = sincos_table((n & 2) ? 1 : 0);
+    return sinf_poly(x * s, x * x, &t, n ^ 1);
 }
 
 // ---------------------------------------------------------------- RNG (rng.h:8-59)

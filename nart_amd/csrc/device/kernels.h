@@ -114,6 +114,39 @@ __global__ __launch_bounds__(256) void k_latin(RenderArgs A) {
     const_cast<uint32_t*>(A.rng0)[slot] = rng;
 }
 
+// Same computation with the two sample arrays in LDS ([spp][64 lanes], bank = lane, so the
+// random-index swaps are conflict-free); one wave per block, spp <= 256 (128 KiB of LDS).
+__global__ __launch_bounds__(64) void k_latin_lds(RenderArgs A) {
+    extern __shared__ __attribute__((aligned(16))) float s_lat[];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t slot = blockIdx.x * 64 + lane;
+    if (slot >= A.n_slots) return;
+    const uint32_t n = A.spp;
+    float* xs = s_lat + lane;
+    float* ys = s_lat + (size_t)n * 64 + lane;
+    uint32_t xy = A.slot_xy[slot];
+    uint32_t x = xy & 0xFFFFu, y = xy >> 16;
+    uint32_t rng = (y * A.totalW + x) + 2463534242u;
+    const float inv = 1.f / (float)n;
+    for (uint32_t i = 0; i < n; ++i) {
+        xs[i * 64] = ((float)i + rng_float(rng)) * inv;
+        ys[i * 64] = ((float)i + rng_float(rng)) * inv;
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t c = rng_int(rng, n - 1 - i);
+        float t = xs[i * 64];
+        xs[i * 64] = xs[c * 64];
+        xs[c * 64] = t;
+        c = rng_int(rng, n - 1 - i);
+        t = ys[i * 64];
+        ys[i * 64] = ys[c * 64];
+        ys[c * 64] = t;
+    }
+    float2* s = const_cast<float2*>(A.samples) + (size_t)slot * n;
+    for (uint32_t i = 0; i < n; ++i) s[i] = make_float2(xs[i * 64], ys[i * 64]);
+    const_cast<uint32_t*>(A.rng0)[slot] = rng;
+}
+
 enum { ST_EXT = 0, ST_SH1 = 1, ST_SH2 = 2 };
 
 // ---------------------------------------------------------------- path tracing megakernel
@@ -371,37 +404,44 @@ struct SplatArgs {
     const float* table;           // [64] Gaussian filter table
     uint32_t n_buckets, spp, B, fb, tile, nbx, totalW, totalH;
     float fw;
+    float invB, invFw;            // exact reciprocals when B / fw are powers of two, else 0
 };
+
+// a / b, or a * (1/b) when 1/b is an exact power of two (bit-identical, avoids the
+// correctly-rounded division sequence)
+ND float div_exact(float a, float b, float inv) { return inv != 0.f ? a * inv : a / b; }
 
 // Exact AddSample test: does this sample's splat loop (render.cpp:27-68) visit tile pixel
 // (tx, ty)?  If so, return the filter weight it adds there.
-ND bool splat_hits(const SplatArgs& A, float scx, float scy, uint32_t tx, uint32_t ty, float& w) {
+//
+// With mx = glm::mod(sc - fb, B) = a - B*k, k = floor(a / B) (a = sc - fb), every term of
+// tileX(x) = floor(((x + 0.5) - sc) + mx + fb) is exact for coordinates < 2^22 (Sterbenz
+// subtraction, an integer multiple of B, a half-integer sum), so tileX(x) = x - B*k exactly and
+// the splat column that lands on tile column tx is x = tx + B*k.  k is the bucket column of the
+// sample, or the next one when x + u rounds up to the bucket edge (the reference then writes the
+// contribution near the tile's origin; so does this).
+ND bool splat_hits(const SplatArgs& A, const float* table, float scx, float scy, uint32_t tx, uint32_t ty, float& w) {
     const float fw = A.fw, fb = (float)A.fb, Bf = (float)A.B;
-    uint32_t x0 = f2u32(floorf(scx - fw)), x1 = f2u32(ceilf(scx + fw));
-    uint32_t y0 = f2u32(floorf(scy - fw)), y1 = f2u32(ceilf(scy + fw));
-    float mx = gmod(scx - fb, Bf), my = gmod(scy - fb, Bf);
-    // tileX(x) = floor(((x + 0.5) - scx) + mx + fb) is x - const for all x of the loop;
-    // solve for x, then verify exactly.
-    float dx0 = ((float)x0 + 0.5f) - scx;
-    uint32_t t0 = f2u32(floorf(dx0 + mx + fb));
-    uint32_t xs = x0 + (tx - t0);
-    if (xs < x0 || xs >= x1) return false;
-    float distX = ((float)xs + 0.5f) - scx;
-    if (f2u32(floorf(distX + mx + fb)) != tx) return false;
-    float dy0 = ((float)y0 + 0.5f) - scy;
-    uint32_t u0 = f2u32(floorf(dy0 + my + fb));
-    uint32_t ys = y0 + (ty - u0);
-    if (ys < y0 || ys >= y1) return false;
-    float distY = ((float)ys + 0.5f) - scy;
-    if (f2u32(floorf(distY + my + fb)) != ty) return false;
-    float dist = sqrtf(distX * distX + distY * distY);
-    uint32_t fi = f2u8((dist / fw) * 64);
+    const uint32_t x0 = (uint32_t)floorf(scx - fw), x1 = (uint32_t)ceilf(scx + fw);
+    const uint32_t y0 = (uint32_t)floorf(scy - fw), y1 = (uint32_t)ceilf(scy + fw);
+    const uint32_t kx = (uint32_t)floorf(div_exact(scx - fb, Bf, A.invB));
+    const uint32_t ky = (uint32_t)floorf(div_exact(scy - fb, Bf, A.invB));
+    const uint32_t xs = tx + A.B * kx, ys = ty + A.B * ky;
+    const bool hit = xs >= x0 && xs < x1 && ys >= y0 && ys < y1;
+    const float distX = ((float)xs + 0.5f) - scx;
+    const float distY = ((float)ys + 0.5f) - scy;
+    const float dist = sqrtf(distX * distX + distY * distY);
+    // static_cast<uint8_t>(float) on x86-64: truncate to int, keep the low byte
+    uint32_t fi = (uint32_t)(int32_t)(div_exact(dist, fw, A.invFw) * 64) & 0xFFu;
     fi = (63u < fi) ? 63u : fi;
-    w = A.table[fi];
-    return true;
+    w = table[fi];
+    return hit;
 }
 
 __global__ __launch_bounds__(256) void k_splat(SplatArgs A) {
+    __shared__ float s_table[64];
+    if (threadIdx.x < 64) s_table[threadIdx.x] = A.table[threadIdx.x];
+    __syncthreads();
     const uint32_t tpx = A.tile * A.tile;
     const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (uint64_t)A.n_buckets * tpx) return;
@@ -413,14 +453,18 @@ __global__ __launch_bounds__(256) void k_splat(SplatArgs A) {
     const uint32_t x1 = min(A.B * (bx + 1), A.totalW), y1 = min(A.B * (by + 1), A.totalH);
     const int bw = (int)(x1 - x0), bh = (int)(y1 - y0);
     const uint32_t base = A.bucket_base[bi];
-    const int r = (int)ceilf(A.fw) + 2;
-    // candidate source pixels: geometric neighbourhood plus the last row/column, whose
-    // samples can wrap onto the next bucket's origin through glm::mod (render.cpp:52-61)
+    // Candidate source pixels.  A sample of bucket-local column S has sc - x0 in [S+fb, S+fb+1],
+    // so its splat columns span [S+fb-ceil(fw), S+fb+1+fw): tile column tx can only be reached
+    // from S in [tx-fb-ceil(fw), tx-fb+ceil(fw)].  Samples of the last column can also wrap to
+    // the next bucket origin (splat_hits) and then reach tx <= fb+ceil(fw).  Same for rows.
+    const int r = (int)ceilf(A.fw);
     const int sxlo = max(0, (int)tx - (int)A.fb - r), sxhi = min(bw - 1, (int)tx - (int)A.fb + r);
     const int sylo = max(0, (int)ty - (int)A.fb - r), syhi = min(bh - 1, (int)ty - (int)A.fb + r);
     float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f, ws = 0.f;
-    const int nrow = (syhi >= sylo ? syhi - sylo + 1 : 0) + (bh - 1 > syhi ? 1 : 0);
-    const int ncol = (sxhi >= sxlo ? sxhi - sxlo + 1 : 0) + (bw - 1 > sxhi ? 1 : 0);
+    const bool wrapx = bw == (int)A.B && (int)tx <= (int)A.fb + r + 1 && bw - 1 > sxhi;
+    const bool wrapy = bh == (int)A.B && (int)ty <= (int)A.fb + r + 1 && bh - 1 > syhi;
+    const int nrow = (syhi >= sylo ? syhi - sylo + 1 : 0) + (wrapy ? 1 : 0);
+    const int ncol = (sxhi >= sxlo ? sxhi - sxlo + 1 : 0) + (wrapx ? 1 : 0);
     for (int ri = 0; ri < nrow; ++ri) {
         const int sy = (sylo + ri <= syhi) ? sylo + ri : bh - 1;
         const float fy = (float)(y0 + (uint32_t)sy + A.fb);
@@ -430,10 +474,26 @@ __global__ __launch_bounds__(256) void k_splat(SplatArgs A) {
             const uint64_t slot = base + (uint64_t)sy * bw + sx;
             const float2* sp = A.samples + slot * A.spp;
             const float4* lp = A.Lout + slot * A.spp;
-            for (uint32_t i = 0; i < A.spp; ++i) {
+            uint32_t i = 0;
+            // 4 samples per step: all loads issued up front, adds applied in sample order
+            for (; (A.spp & 1u) == 0 && i + 4 <= A.spp; i += 4) {
+                float4 uv01 = *reinterpret_cast<const float4*>(sp + i);
+                float4 uv23 = *reinterpret_cast<const float4*>(sp + i + 2);
+                float4 L0 = lp[i], L1 = lp[i + 1], L2 = lp[i + 2], L3 = lp[i + 3];
+                float w0, w1, w2, w3;
+                bool h0 = splat_hits(A, s_table, fx + uv01.x, fy + uv01.y, tx, ty, w0);
+                bool h1 = splat_hits(A, s_table, fx + uv01.z, fy + uv01.w, tx, ty, w1);
+                bool h2 = splat_hits(A, s_table, fx + uv23.x, fy + uv23.y, tx, ty, w2);
+                bool h3 = splat_hits(A, s_table, fx + uv23.z, fy + uv23.w, tx, ty, w3);
+                if (h0) { c0 += L0.x * w0; c1 += L0.y * w0; c2 += L0.z * w0; c3 += L0.w * w0; ws += w0; }
+                if (h1) { c0 += L1.x * w1; c1 += L1.y * w1; c2 += L1.z * w1; c3 += L1.w * w1; ws += w1; }
+                if (h2) { c0 += L2.x * w2; c1 += L2.y * w2; c2 += L2.z * w2; c3 += L2.w * w2; ws += w2; }
+                if (h3) { c0 += L3.x * w3; c1 += L3.y * w3; c2 += L3.z * w3; c3 += L3.w * w3; ws += w3; }
+            }
+            for (; i < A.spp; ++i) {
                 float2 uv = sp[i];
                 float w;
-                if (splat_hits(A, fx + uv.x, fy + uv.y, tx, ty, w)) {
+                if (splat_hits(A, s_table, fx + uv.x, fy + uv.y, tx, ty, w)) {
                     float4 Lv = lp[i];
                     c0 += Lv.x * w;
                     c1 += Lv.y * w;

@@ -181,6 +181,18 @@ void dispatch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     else c ? launch_render<32, true>(ctx, a, st) : launch_render<32, false>(ctx, a, st);
 }
 
+// LatinSquare per traced pixel: LDS variant up to 256 spp, global-memory variant beyond.
+int launch_latin(nart_ctx* ctx, const RenderArgs& ra, hipStream_t st) {
+    if (ra.spp <= 256) {
+        size_t lds = (size_t)ra.spp * 2 * 64 * sizeof(float);
+        hipLaunchKernelGGL(k_latin_lds, dim3((ra.n_slots + 63) / 64), dim3(64), lds, st, ra);
+    } else {
+        hipLaunchKernelGGL(k_latin, dim3((ra.n_slots + 255) / 256), dim3(256), 0, st, ra);
+    }
+    HIPCHK(hipGetLastError());
+    return NART_OK;
+}
+
 // Render a bucket list into device tiles (list order).  Shared by all entry points.
 int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* ids, uint32_t n, float* d_tiles,
                    hipStream_t st, nart_render_stats* stats) {
@@ -204,7 +216,7 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
     }
     const size_t limit = batch_slot_limit(p->spp);
     const uint32_t tpx = g.tile_size * g.tile_size;
-    double kernel_ms = 0.0, splat_ms = 0.0;
+    double kernel_ms = 0.0, splat_ms = 0.0, latin_ms = 0.0;
     uint32_t launches = 0;
     uint64_t traced = 0, counted = 0;
     uint32_t b0 = 0;
@@ -251,8 +263,9 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         ra.stack_depth = ctx->stack_depth;
         ra.gamma = p->roughening_factor * p->roughening_factor;
         ra.counters = ctx->d_counters;
-        hipLaunchKernelGGL(k_latin, dim3((nslots + 255) / 256), dim3(256), 0, st, ra);
-        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(ctx->ev[3], st));
+        rc = launch_latin(ctx, ra, st);
+        if (rc) return rc;
         HIPCHK(hipEventRecord(ctx->ev[0], st));
         dispatch_render(ctx, ra, st);
         HIPCHK(hipGetLastError());
@@ -273,6 +286,12 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         sa.totalW = g.total_width;
         sa.totalH = g.total_height;
         sa.fw = p->filter_width;
+        sa.invB = (p->bucket_size & (p->bucket_size - 1)) == 0 ? 1.f / (float)p->bucket_size : 0.f;
+        {
+            int ex = 0;
+            float m = std::frexp(p->filter_width, &ex);
+            sa.invFw = (m == 0.5f) ? 1.f / p->filter_width : 0.f;
+        }
         uint64_t nthreads = (uint64_t)nbk * tpx;
         hipLaunchKernelGGL(k_splat, dim3((uint32_t)((nthreads + 255) / 256)), dim3(256), 0, st, sa);
         HIPCHK(hipGetLastError());
@@ -283,12 +302,15 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         kernel_ms += ms;
         HIPCHK(hipEventElapsedTime(&ms, ctx->ev[1], ctx->ev[2]));
         splat_ms += ms;
+        HIPCHK(hipEventElapsedTime(&ms, ctx->ev[3], ctx->ev[0]));
+        latin_ms += ms;
         ++launches;
         b0 = b1;
     }
     if (stats) {
         stats->kernel_ms += kernel_ms;
         stats->splat_ms += splat_ms;
+        stats->latin_ms += latin_ms;
         stats->kernel_launches += launches;
         stats->traced_samples += traced;
         stats->samples += counted * p->spp;
@@ -326,6 +348,10 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
         return code;
     };
     if (hipSetDevice(device_id) != hipSuccess) return bail(NART_E_HIP);
+    // dynamic LDS above the 64 KiB default: LatinSquare arrays (128 KiB at 256 spp)
+    if (hipFuncSetAttribute((const void*)k_latin_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+        hipSuccess)
+        return bail(NART_E_HIP);
     for (uint32_t l = 0; l < blob->num_lights; ++l)
         if (blob->lights[l].type == NART_LIGHT_ENVIRONMENT) {
             ctx->err = "environment lights are not supported on the device yet";
@@ -536,7 +562,8 @@ int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t
     ra.stack_depth = ctx->stack_depth;
     ra.gamma = p->roughening_factor * p->roughening_factor;
     ra.counters = ctx->d_counters;
-    hipLaunchKernelGGL(k_latin, dim3((n + 255) / 256), dim3(256), 0, 0, ra);
+    rc = launch_latin(ctx, ra, 0);
+    if (rc) return rc;
     dispatch_render(ctx, ra, 0);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(out, ctx->d_L, (size_t)n * p->spp * sizeof(float4), hipMemcpyDeviceToHost));

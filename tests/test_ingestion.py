@@ -1,0 +1,149 @@
+"""Host surface of the drop-in: JSON scene + .geo ingestion, session/CLI resolution, filter
+table, EXR output.  Reference: src/core/scene.cpp, src/core/render.cpp:208-414, render.h."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import nart_amd
+from nart_amd import scenes
+
+
+def test_glass_sphere_counts(glass_scene):
+    c = glass_scene.counts()
+    assert c == {"triangles": 2560, "meshes": 3, "materials": 3, "lights": 1, "textures": 0}
+
+
+def test_sessions_from_json(glass_scene):
+    (p,) = nart_amd.load_sessions(glass_scene.path)
+    assert (p.image_width, p.image_height, p.bucket_size, p.spp, p.bounces) == (1280, 720, 16, 64, 10)
+    assert p.filter_width == 2.0 and p.roughening_factor == np.float32(0.2)
+
+
+def test_cli_overrides_json(glass_scene):
+    cli = nart_amd.parse_args(["nart", glass_scene.path, "out", "-w", "256", "-h", "128", "-s", "16", "-o", "3",
+                               "-b", "8", "-f", "1.5", "-r", "1.7"])
+    (p,) = nart_amd.load_sessions(glass_scene.path, cli)
+    assert (p.image_width, p.image_height, p.spp, p.bounces, p.bucket_size) == (256, 128, 16, 3, 8)
+    assert p.filter_width == 1.5
+    assert p.roughening_factor == np.float32(1.7)  # CLI value is not clamped (render.cpp:317-323)
+
+
+def test_cli_long_flags_and_errors(glass_scene):
+    p = nart_amd.parse_args(["nart", "s", "o", "--imageWidth", "32", "--spp", "3x"])  # stoi prefix parse
+    assert p.image_width == 32 and p.spp == 3
+    for bad in (["nart", "s", "o", "-q", "1"], ["nart", "s", "o", "-w", "abc"], ["nart", "s", "o", "-w"]):
+        with pytest.raises(nart_amd.NartError):
+            nart_amd.parse_args(bad)
+
+
+def _scene_file(tmp_path, session=None, material=None, light=None, extra=None):
+    d = str(tmp_path)
+    scenes.write_geo(os.path.join(d, "q.geo"), [[0, 1, 2, 3]], [(0, 0, 0), (1, 0, 0), (1, 1, 0), (0, 1, 0)],
+                     [(0, 0, 1)], [[0, 0, 0, 0]])
+    sc = {"renderSessions": [session if session is not None else {}],
+          "camera": {"fov": 20, "transform": [1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 3, 0, 0, 0, 1]},
+          "meshes": [{"filePath": os.path.join(d, "q.geo"),
+                      "material": material or {"type": "lambert", "rho_d": [1.5, 0.5, 1]}}],
+          "lights": [light or {"type": "disk", "radius": 0.5, "Le": [1, 1, 1], "intensity": 5}]}
+    sc.update(extra or {})
+    path = os.path.join(d, "s.json")
+    json.dump(sc, open(path, "w"))
+    return path
+
+
+def test_session_defaults_and_clamp(tmp_path):
+    path = _scene_file(tmp_path, session={"rougheningFactor": 3.0})
+    (p,) = nart_amd.load_sessions(path)
+    assert (p.image_width, p.image_height, p.bucket_size, p.spp, p.bounces) == (64, 64, 16, 1, 10)
+    assert p.filter_width == 1.0
+    assert p.roughening_factor == 1.0  # JSON value clamped to [0,1] (render.cpp:375-378)
+
+
+def test_multiple_sessions(tmp_path):
+    path = _scene_file(tmp_path)
+    sc = json.load(open(path))
+    sc["renderSessions"] = [{"spp": 2}, {"spp": 3, "integrator": "volume"}, {}]
+    json.dump(sc, open(path, "w"))
+    ps = nart_amd.load_sessions(path)
+    assert [p.spp for p in ps] == [2, 3, 1]
+    assert [p.integrator for p in ps] == [0, 1, 0]
+
+
+def test_constant_pattern_object_is_rejected(tmp_path):
+    """Q9: {"type": "constant"} falls into the if/else-abort chain (scene.cpp:352-374)."""
+    path = _scene_file(tmp_path, material={"type": "lambert", "rho_d": {"type": "constant", "value": [1, 1, 1]}})
+    with pytest.raises(nart_amd.NartError):
+        nart_amd.Scene(path)
+
+
+def test_unknown_material_is_rejected(tmp_path):
+    with pytest.raises(nart_amd.NartError):
+        nart_amd.Scene(_scene_file(tmp_path, material={"type": "velvet"}))
+
+
+def test_missing_mesh_file(tmp_path):
+    path = _scene_file(tmp_path)
+    sc = json.load(open(path))
+    sc["meshes"][0]["filePath"] = os.path.join(str(tmp_path), "nope.geo")
+    json.dump(sc, open(path, "w"))
+    with pytest.raises(nart_amd.NartError) as e:
+        nart_amd.Scene(path)
+    assert e.value.code == -2
+
+
+def test_fan_triangulation_and_default_uvs(tmp_path):
+    sc = nart_amd.Scene(_scene_file(tmp_path))
+    assert sc.counts()["triangles"] == 2  # one quad -> fan of 2 (scene.cpp:274-282)
+
+
+def test_filter_table():
+    t = nart_amd.filter_table()
+    sigma = np.float32(21.0)
+    assert t[63] == 0.0
+    assert abs(t[0] - 1 / np.sqrt(2 * np.pi * sigma * sigma)) < 1e-8
+    assert np.all(np.diff(t) <= 0)
+
+
+def test_half_conversion_matches_ieee_rne():
+    lib = nart_amd.scene_lib()
+    rng = np.random.default_rng(3)
+    vals = np.concatenate([rng.standard_normal(20000).astype(np.float32) * 100,
+                           np.float32([0, -0.0, 65504, 65520, 1e-8, 6e-5, np.inf, -np.inf, 2.0 ** -24, 3 * 2.0 ** -25])])
+    got = np.array([lib.nart_float_to_half(float(v)) for v in vals], np.uint16)
+    want = vals.astype(np.float16).view(np.uint16)
+    assert np.array_equal(got, want)
+    back = np.array([lib.nart_half_to_float(int(h)) for h in want], np.float32)
+    assert np.array_equal(back, want.view(np.float16).astype(np.float32))
+
+
+@pytest.mark.parametrize("compression", [0, 3])
+def test_exr_roundtrip(tmp_path, compression):
+    p = nart_amd.default_params()
+    p.image_width, p.image_height, p.bucket_size, p.spp, p.bounces = 37, 21, 16, 1, 1
+    p.filter_width, p.roughening_factor = 2.0, 0.0
+    g = nart_amd.session_geometry(p)
+    rng = np.random.default_rng(0)
+    img = rng.random((g.total_height, g.total_width, 5), dtype=np.float32) * 4
+    img[..., 4] += 0.5
+    path = str(tmp_path / "o.exr")
+    nart_amd.write_exr(path, p, img, compression)
+    back = nart_amd.read_exr(path)
+    want = nart_amd.finalize(p, img).astype(np.float16).astype(np.float32)
+    assert back.shape == (21, 37, 4)
+    assert np.array_equal(back, want)
+
+
+def test_reads_reference_style_texture(tmp_path):
+    """ZIP-compressed EXR written by our writer reads back through the texture reader."""
+    p = nart_amd.default_params()
+    p.image_width, p.image_height, p.bucket_size, p.spp, p.bounces = 64, 40, 16, 1, 1
+    p.filter_width, p.roughening_factor = 1.0, 0.0
+    g = nart_amd.session_geometry(p)
+    img = np.ones((g.total_height, g.total_width, 5), np.float32)
+    img[..., 0] = np.linspace(0, 1, g.total_width, dtype=np.float32)[None, :]
+    path = str(tmp_path / "t.exr")
+    nart_amd.write_exr(path, p, img, 3)
+    tex = nart_amd.read_exr(path)
+    assert tex.shape == (40, 64, 4) and tex[..., 3].min() == 1.0
