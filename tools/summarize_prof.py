@@ -1,0 +1,57 @@
+"""Summarise a tools/profile.sh run into profiles/ (committed evidence).
+
+    python tools/summarize_prof.py gpurun_out/prof1 r01
+
+writes profiles/<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats summary),
+profiles/<tag>_pmc.json and profiles/pmc_latest.json (HBM bytes per launch per nart kernel).
+FETCH_SIZE / WRITE_SIZE are KiB (rocprofv3); per MI355X_MICROARCH.md (HBM section) FETCH_SIZE
+reads 1/2 of a wide coalesced streaming read on gfx950 -- the render kernels' reads are not
+wide streaming reads (scattered 8/16-B gathers), so both the raw and the x2-corrected read
+figures are recorded and `hbm_bytes_per_launch` uses the raw (uncalibrated) sum.
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main(src, tag, config="1920x1080x256"):
+    prof = os.path.join(REPO, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(prof, tag + "_kernel_stats.csv"))
+    per = {}
+    for kind in ("fetch", "write"):
+        for r in csv.DictReader(open(os.path.join(src, kind, "run_counter_collection.csv"))):
+            name = r["Kernel_Name"]
+            if "nd::" not in name:
+                continue
+            key = name.split("(")[0].replace("void ", "")
+            d = per.setdefault(key, {"launches": {}, "vgpr": r["VGPR_Count"], "sgpr": r["SGPR_Count"],
+                                     "lds": r["LDS_Block_Size"], "scratch": r["Scratch_Size"]})
+            dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+            d["launches"].setdefault(r["Dispatch_Id"] if kind == "fetch" else None, None)
+            d.setdefault(kind, []).append((float(r["Counter_Value"]), dur))
+    out = {"config": config, "kernels": {}}
+    for k, d in per.items():
+        f = max(d.get("fetch", [(0, 0)]))
+        w = max(d.get("write", [(0, 0)]))
+        out["kernels"][k] = {"fetch_kib": f[0], "write_kib": w[0], "fetch_bytes": f[0] * 1024,
+                             "fetch_bytes_x2_corrected": f[0] * 2048, "write_bytes": w[0] * 1024,
+                             "duration_ms_fetch_pass": f[1], "duration_ms_write_pass": w[1],
+                             "vgpr_count": d["vgpr"], "sgpr_count": d["sgpr"], "lds_bytes": d["lds"],
+                             "scratch_bytes": d["scratch"]}
+    render = [k for k in out["kernels"] if "k_render" in k and "true" not in k]
+    if render:
+        r = out["kernels"][render[0]]
+        out["hbm_bytes_per_launch"] = r["fetch_bytes"] + r["write_bytes"]
+        out["render_kernel"] = render[0]
+    json.dump(out, open(os.path.join(prof, tag + "_pmc.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(prof, "pmc_latest.json"), "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
