@@ -225,7 +225,7 @@ class Scene:
 class HipRenderer:
     """nart_ctx: the scene resident on one GPU; Render()-equivalent entry points."""
 
-    def __init__(self, scene, device=0):
+    def __init__(self, scene, device=0, variant=None):
         self._lib = hip_lib()
         self.scene = scene
         self.device = device
@@ -233,6 +233,12 @@ class HipRenderer:
         rc = self._lib.nart_hip_create(scene.blob, device, ctypes.byref(self._ctx))
         if rc != NART_OK:
             raise NartError(rc, "nart_hip_create failed on device %d" % device)
+        if variant is not None:
+            self.set_variant(variant)
+
+    def set_variant(self, variant):
+        """0 = megakernel, 1 = wavefront (trace/shade over ray queues); identical results."""
+        self._check(self._lib.nart_hip_set_variant(self._ctx, int(variant)))
 
     def _check(self, rc):
         if rc != NART_OK:

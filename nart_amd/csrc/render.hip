@@ -11,7 +11,7 @@
 #include <vector>
 
 #include "../../include/nart_hip.h"
-#include "device/kernels.h"
+#include "device/wavefront.h"
 #include "host/bvh_build.h"
 
 using namespace nd;
@@ -46,6 +46,13 @@ struct nart_ctx {
     size_t cap_slots = 0, cap_samples = 0, cap_buckets = 0;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool events = false;
+    // wavefront variant: path state + queues (one allocation), pinned queue-count readback
+    void* d_wf = nullptr;
+    size_t cap_wf = 0;
+    uint32_t* h_counts = nullptr;
+    hipEvent_t ev_chunk[2] = {nullptr, nullptr};
+    uint32_t wf_grid_trace = 0, wf_grid_shade = 0;
+    uint64_t wf_iterations = 0;
     uint64_t stat_counts[5] = {0, 0, 0, 0, 0};
 };
 
@@ -174,11 +181,125 @@ void launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((k_render<MAXL, COUNT>), grid, block, lds, st, ctx->scene, a);
 }
 
-void dispatch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
+int dispatch_megakernel(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     const bool c = ctx->counters;
     if (a.bounces <= 10) c ? launch_render<10, true>(ctx, a, st) : launch_render<10, false>(ctx, a, st);
     else if (a.bounces <= 16) c ? launch_render<16, true>(ctx, a, st) : launch_render<16, false>(ctx, a, st);
     else c ? launch_render<32, true>(ctx, a, st) : launch_render<32, false>(ctx, a, st);
+    HIPCHK(hipGetLastError());
+    return NART_OK;
+}
+
+// ---------------------------------------------------------------- wavefront variant
+// Carve the path state and queues for n slots out of one allocation (256-B aligned rows).
+int wf_layout(nart_ctx* ctx, uint32_t n, int maxl, WFArgs& w) {
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        size_t o = off;
+        off += (bytes + 255) & ~(size_t)255;
+        return o;
+    };
+    const size_t N = n;
+    size_t o_u = take(N * 16), o_L = take(N * 16), o_beta = take(N * 16), o_misc = take(N * 16);
+    size_t o_c1 = take(N * 16), o_c2 = take(N * 16), o_bk = take(N * 16);
+    size_t o_ro = take(3 * N * 16), o_rd = take(3 * N * 16), o_hit = take(N * 8), o_occ = take(3 * N);
+    size_t o_ln = take(N * 4), o_lid = take((size_t)maxl * N * 4), o_leta = take((size_t)maxl * N * 4);
+    size_t o_rq0 = take(3 * N * 4), o_rq1 = take(3 * N * 4), o_sq0 = take(N * 4), o_sq1 = take(N * 4);
+    size_t o_cnt = take(16);
+    if (off > ctx->cap_wf) {
+        if (ctx->d_wf) hipFree(ctx->d_wf);
+        ctx->d_wf = nullptr;
+        ctx->cap_wf = 0;
+        if (hipMalloc(&ctx->d_wf, off) != hipSuccess) return fail(ctx, NART_E_OOM, "hipMalloc wavefront state");
+        ctx->cap_wf = off;
+    }
+    char* b = static_cast<char*>(ctx->d_wf);
+    WFState& T = w.st;
+    T.u = (uint4*)(b + o_u);
+    T.L = (float4*)(b + o_L);
+    T.beta = (float4*)(b + o_beta);
+    T.misc = (float4*)(b + o_misc);
+    T.c1 = (float4*)(b + o_c1);
+    T.c2 = (float4*)(b + o_c2);
+    T.betak = (float4*)(b + o_bk);
+    T.ray_o = (float4*)(b + o_ro);
+    T.ray_d = (float4*)(b + o_rd);
+    T.hit = (uint2*)(b + o_hit);
+    T.occ = (uint8_t*)(b + o_occ);
+    T.ln = (uint32_t*)(b + o_ln);
+    T.lid = (uint32_t*)(b + o_lid);
+    T.leta = (float*)(b + o_leta);
+    w.rq[0] = (uint32_t*)(b + o_rq0);
+    w.rq[1] = (uint32_t*)(b + o_rq1);
+    w.sq[0] = (uint32_t*)(b + o_sq0);
+    w.sq[1] = (uint32_t*)(b + o_sq1);
+    w.counts = (uint32_t*)(b + o_cnt);
+    return NART_OK;
+}
+
+// Persistent grids: as many resident blocks as the occupancy calculator allows on every CU.
+template <int MAXL, bool COUNT>
+int wf_grids(nart_ctx* ctx, size_t lds) {
+    int cus = 0, bt = 0, bs = 0;
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bt, (const void*)k_wf_trace<COUNT>, 256, lds));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bs, (const void*)k_wf_shade<MAXL>, 256, 0));
+    ctx->wf_grid_trace = (uint32_t)std::max(1, cus * std::max(bt, 1));
+    ctx->wf_grid_shade = (uint32_t)std::max(1, cus * std::max(bs, 1));
+    return NART_OK;
+}
+
+// Iterate trace/shade until every slot has retired.  Queue counts are read back in chunks of
+// iterations, one chunk behind the launches, so the GPU never waits for the host.
+template <int MAXL, bool COUNT>
+int run_wavefront(nart_ctx* ctx, const RenderArgs& ra, hipStream_t st) {
+    WFArgs w;
+    w.R = ra;
+    int rc = wf_layout(ctx, ra.n_slots, MAXL, w);
+    if (rc) return rc;
+    const size_t lds = (size_t)ctx->stack_depth * 256 * 8;
+    if ((rc = wf_grids<MAXL, COUNT>(ctx, lds))) return rc;
+    if (!ctx->h_counts) {
+        HIPCHK(hipHostMalloc((void**)&ctx->h_counts, 4 * sizeof(uint32_t), hipHostMallocDefault));
+        for (auto& e : ctx->ev_chunk) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    HIPCHK(hipMemsetAsync(w.counts, 0, 4 * sizeof(uint32_t), st));
+    const uint32_t init_grid = std::min<uint32_t>((ra.n_slots + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_wf_init, dim3(init_grid), dim3(256), 0, st, ctx->scene, w);
+    HIPCHK(hipGetLastError());
+    if (ra.bounces == 0) return NART_OK;
+    // every shade advances each live slot by one bounce or one sample, plus one final resolve
+    const uint64_t max_it = (uint64_t)ra.spp * (ra.bounces + 1) + 2;
+    const uint32_t K = 8;
+    uint32_t it = 0;
+    for (uint32_t chunk = 0;; ++chunk) {
+        for (uint32_t j = 0; j < K; ++j, ++it) {
+            hipLaunchKernelGGL((k_wf_trace<COUNT>), dim3(ctx->wf_grid_trace), dim3(256), lds, st, ctx->scene, w, it);
+            hipLaunchKernelGGL((k_wf_shade<MAXL>), dim3(ctx->wf_grid_shade), dim3(256), 0, st, ctx->scene, w, it);
+        }
+        HIPCHK(hipGetLastError());
+        // slots queued for iteration `it` (written by shade(it - 1))
+        HIPCHK(hipMemcpyAsync(&ctx->h_counts[chunk & 1], &w.counts[2 + (it & 1)], 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipEventRecord(ctx->ev_chunk[chunk & 1], st));
+        if (chunk > 0) {
+            HIPCHK(hipEventSynchronize(ctx->ev_chunk[(chunk - 1) & 1]));
+            if (ctx->h_counts[(chunk - 1) & 1] == 0) break;
+        }
+        if (it > max_it + 2 * K) return fail(ctx, NART_E_HIP, "wavefront queues did not drain");
+    }
+    ctx->wf_iterations += it;
+    return NART_OK;
+}
+
+int dispatch_wavefront(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
+    const bool c = ctx->counters;
+    if (a.bounces <= 10) return c ? run_wavefront<10, true>(ctx, a, st) : run_wavefront<10, false>(ctx, a, st);
+    if (a.bounces <= 16) return c ? run_wavefront<16, true>(ctx, a, st) : run_wavefront<16, false>(ctx, a, st);
+    return c ? run_wavefront<32, true>(ctx, a, st) : run_wavefront<32, false>(ctx, a, st);
+}
+
+int dispatch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
+    return ctx->variant == 1 ? dispatch_wavefront(ctx, a, st) : dispatch_megakernel(ctx, a, st);
 }
 
 // LatinSquare per traced pixel: LDS variant up to 256 spp, global-memory variant beyond.
@@ -267,8 +388,8 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         rc = launch_latin(ctx, ra, st);
         if (rc) return rc;
         HIPCHK(hipEventRecord(ctx->ev[0], st));
-        dispatch_render(ctx, ra, st);
-        HIPCHK(hipGetLastError());
+        rc = dispatch_render(ctx, ra, st);
+        if (rc) return rc;
         HIPCHK(hipEventRecord(ctx->ev[1], st));
         SplatArgs sa;
         sa.bucket_ids = ctx->d_bucket_ids;
@@ -337,6 +458,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     if (!ctx) return NART_E_OOM;
     *out = nullptr;
     ctx->device = device_id;
+    if (const char* v = std::getenv("NART_VARIANT")) ctx->variant = std::atoi(v) == 1 ? 1 : 0;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device_id || device_id < 0) {
         delete ctx;
@@ -446,11 +568,15 @@ void nart_hip_destroy(nart_ctx* ctx) {
     hipSetDevice(ctx->device);
     void* bufs[] = {ctx->d_nodes, ctx->d_tri_isect, ctx->d_tris, ctx->d_tri_mesh, ctx->d_meshes, ctx->d_mats,
                     ctx->d_lights, ctx->d_texs, ctx->d_tex_pool, ctx->d_slot_xy, ctx->d_rng, ctx->d_samples,
-                    ctx->d_L, ctx->d_bucket_ids, ctx->d_bucket_base, ctx->d_table, ctx->d_counters};
+                    ctx->d_L, ctx->d_bucket_ids, ctx->d_bucket_base, ctx->d_table, ctx->d_counters, ctx->d_wf};
     for (void* b : bufs)
         if (b) hipFree(b);
     if (ctx->events)
         for (auto& e : ctx->ev) hipEventDestroy(e);
+    if (ctx->h_counts) {
+        hipHostFree(ctx->h_counts);
+        for (auto& e : ctx->ev_chunk) hipEventDestroy(e);
+    }
     delete ctx;
 }
 
@@ -464,7 +590,8 @@ int nart_hip_set_counters(nart_ctx* ctx, int enable) {
 
 int nart_hip_set_variant(nart_ctx* ctx, int variant) {
     if (!ctx) return NART_E_INVALID;
-    if (variant != 0) return fail(ctx, NART_E_UNSUPPORTED, "only the megakernel variant (0) is built");
+    if (variant != 0 && variant != 1)
+        return fail(ctx, NART_E_UNSUPPORTED, "variant must be 0 (megakernel) or 1 (wavefront)");
     ctx->variant = variant;
     return NART_OK;
 }
@@ -564,8 +691,8 @@ int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t
     ra.counters = ctx->d_counters;
     rc = launch_latin(ctx, ra, 0);
     if (rc) return rc;
-    dispatch_render(ctx, ra, 0);
-    HIPCHK(hipGetLastError());
+    rc = dispatch_render(ctx, ra, 0);
+    if (rc) return rc;
     HIPCHK(hipMemcpy(out, ctx->d_L, (size_t)n * p->spp * sizeof(float4), hipMemcpyDeviceToHost));
     return NART_OK;
 }

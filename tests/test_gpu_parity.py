@@ -31,9 +31,12 @@ def _report(a, b):
     return "%d of %d floats differ, max abs diff %g" % (int(ne.sum()), ne.size, float(np.nanmax(np.abs(a - b))))
 
 
-@pytest.fixture(scope="module")
-def glass_gpu(gpu, glass_scene):
-    return nart_amd.HipRenderer(glass_scene)
+VARIANTS = [0, 1]  # megakernel, wavefront
+
+
+@pytest.fixture(scope="module", params=VARIANTS, ids=["megakernel", "wavefront"])
+def glass_gpu(request, gpu, glass_scene):
+    return nart_amd.HipRenderer(glass_scene, variant=request.param)
 
 
 @pytest.fixture(scope="module")
@@ -93,10 +96,20 @@ def test_framebuffer_ragged_buckets(glass_gpu, glass_oracle, glass_scene):
     assert _bits_equal(g, r), _report(g, r)
 
 
-def test_cornell_box(gpu, cornell_scene):
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_cornell_box(gpu, cornell_scene, variant):
     p = _params(cornell_scene, 96, 64, 8)
-    g = nart_amd.HipRenderer(cornell_scene).render(p)
+    g = nart_amd.HipRenderer(cornell_scene, variant=variant).render(p)
     r = oracle.Oracle(cornell_scene).render(p)
+    assert _bits_equal(g, r), _report(g, r)
+
+
+@pytest.mark.parametrize("bounces", [0, 1, 2, 12, 20])
+def test_bounce_limits(glass_gpu, glass_oracle, glass_scene, bounces):
+    """Bounce caps (pathintegrator.cpp:165): none, shallow, and the 16/32-entry list builds."""
+    p = _params(glass_scene, 24, 20, 5, bucket_size=8, bounces=bounces)
+    g = glass_gpu.render(p)
+    r = glass_oracle.render(p)
     assert _bits_equal(g, r), _report(g, r)
 
 
