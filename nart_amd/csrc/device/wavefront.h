@@ -1,9 +1,9 @@
 // Wavefront variant of the path tracer: ray queues + path state in HBM.
 //
-// Per iteration two kernels run over compacted queues:
+// Per iteration two kernels run:
 //   k_wf_trace  every queued ray (extension = closest hit, shadow = any hit) of the iteration
 //               through one traversal loop; writes hit records / occlusion bytes per slot.
-//   k_wf_shade  every queued slot: (a) adds last bounce's deferred EstimateDirect term using the
+//   k_wf_shade  every live slot, in slot order: (a) adds last bounce's deferred EstimateDirect term using the
 //               shadow results, (b) stores the sample that ended last bounce and starts the one
 //               whose camera ray was just traced, (c) shades this bounce's hit (BSDF,
 //               EstimateDirect, continuation, Russian roulette) and emits the next rays
@@ -31,6 +31,7 @@ namespace nd {
 #define WF_FINISH (1u << 12)      // the current sample ended: store it before shading the new ray
 #define WF_RETIRE (1u << 13)      // ... and it was the pixel's last sample
 #define WF_NEXT_LIGHT (1u << 14)  // the next sample's camera ray hit a light first
+#define WF_DEAD (1u << 15)        // all samples of the pixel stored
 
 enum { RK_EXT = 0, RK_SH1 = 1, RK_SH2 = 2 };
 
@@ -54,9 +55,9 @@ struct WFState {
 struct WFArgs {
     RenderArgs R;
     WFState st;
-    uint32_t* rq[2];   // ray queues by iteration parity: slot << 2 | kind
-    uint32_t* sq[2];   // slot queues by iteration parity
-    uint32_t* counts;  // [p] rays, [2 + p] slots in queue p
+    uint32_t* rq_ext[2];  // extension-ray queues by iteration parity: slot
+    uint32_t* rq_sh[2];   // shadow-ray queues by iteration parity: slot << 2 | kind
+    uint32_t* counts;     // [p] extension rays, [2 + p] shadow rays, [4 + p] live slots of parity p
 };
 
 // Wave-aggregated append: each active lane reserves `n` consecutive entries; one atomic per wave.
@@ -134,6 +135,7 @@ __global__ __launch_bounds__(256) void k_wf_init(DScene S, WFArgs A) {
         if (slot < R.n_slots && R.bounces == 0) {
             // every sample ends before its first light loop (pathintegrator.cpp:165)
             for (uint32_t s = 0; s < R.spp; ++s) R.Lout[(size_t)slot * R.spp + s] = make_float4(0.f, 0.f, 0.f, 0.f);
+            A.st.u[slot] = make_uint4(0u, R.spp, 0u, WF_DEAD);
         }
         if (live) {
             f3 o, d, Le;
@@ -148,11 +150,9 @@ __global__ __launch_bounds__(256) void k_wf_init(DScene S, WFArgs A) {
             A.st.ln[slot] = 0;
         }
         const uint32_t ri = wave_append(&A.counts[0], live ? 1u : 0u);
-        const uint32_t si = wave_append(&A.counts[2], live ? 1u : 0u);
-        if (live) {
-            A.rq[0][ri] = (slot << 2) | RK_EXT;
-            A.sq[0][si] = slot;
-        }
+        if (live) A.rq_ext[0][ri] = slot;
+        const uint32_t nlive = wave_sum(live ? 1u : 0u);
+        if (__lane_id() == 0 && nlive) atomicAdd(&A.counts[4], nlive);
     }
 }
 
@@ -166,14 +166,17 @@ __global__ __launch_bounds__(256) void k_wf_trace(DScene S, WFArgs A, uint32_t i
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         A.counts[nxt] = 0;  // queues of the next iteration, filled by k_wf_shade(it)
         A.counts[2 + nxt] = 0;
+        A.counts[4 + nxt] = 0;
     }
-    const uint32_t n = A.counts[cur];
+    // extension rays first, then shadow rays: a wave holds one query type except at the seam
+    const uint32_t ne = A.counts[cur];
+    const uint32_t n = ne + A.counts[2 + cur];
     const uint32_t gsize = gridDim.x * blockDim.x;
     const size_t N = A.R.n_slots;
     TraceCounters cnt = {0u, 0u};
     uint32_t n_ext = 0, n_sh = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gsize) {
-        const uint32_t tag = A.rq[cur][i];
+        const uint32_t tag = i < ne ? (A.rq_ext[cur][i] << 2) : A.rq_sh[cur][i - ne];
         const uint32_t slot = tag >> 2, kind = tag & 3u;
         const float4 o = A.st.ray_o[kind * N + slot];
         const float4 d = A.st.ray_d[kind * N + slot];
@@ -205,12 +208,11 @@ __global__ __launch_bounds__(256) void k_wf_trace(DScene S, WFArgs A, uint32_t i
 // Returns the rays emitted (bit 0 extension, bit 1 shadow 1, bit 2 shadow 2); their origin,
 // direction and bound are already stored in the slot's ray rows.
 template <int MAXL>
-ND uint32_t shade_slot(const DScene& S, const WFArgs& A, uint32_t slot) {
+ND uint32_t shade_slot(const DScene& S, const WFArgs& A, uint32_t slot, const uint4 u) {
     const RenderArgs& R = A.R;
     const WFState& T = A.st;
     const size_t N = R.n_slots;
     const float nL = (float)S.num_lights;
-    const uint4 u = T.u[slot];
     uint32_t rng = u.x, s = u.y, bounce = u.z, fl = u.w;
     const float4 L4 = T.L[slot], B4 = T.beta[slot], M4 = T.misc[slot];
     f3 L = F3(L4.x, L4.y, L4.z), beta = F3(B4.x, B4.y, B4.z), Le = F3(M4.x, M4.y, M4.z);
@@ -237,7 +239,10 @@ ND uint32_t shade_slot(const DScene& S, const WFArgs& A, uint32_t slot) {
     if (fl & WF_FINISH) {
         R.Lout[(size_t)slot * R.spp + s] = make_float4(L.x, L.y, L.z, alpha);
         ++s;
-        if (fl & WF_RETIRE) return 0u;  // pixel done; its state is never read again
+        if (fl & WF_RETIRE) {  // pixel done
+            T.u[slot] = make_uint4(rng, s, bounce, WF_DEAD);
+            return 0u;
+        }
         const bool lh = (fl & WF_NEXT_LIGHT) != 0;
         L = F3(0.f, 0.f, 0.f);
         alpha = lh ? 1.f : 0.f;
@@ -410,7 +415,10 @@ ND uint32_t shade_slot(const DScene& S, const WFArgs& A, uint32_t slot) {
         } else {
             R.Lout[(size_t)slot * R.spp + s] = make_float4(L.x, L.y, L.z, alpha);
             ++s;
-            if (s >= R.spp) return 0u;  // pixel done
+            if (s >= R.spp) {  // pixel done
+                T.u[slot] = make_uint4(rng, s, bounce, WF_DEAD);
+                return 0u;
+            }
             f3 o, d, LeN;
             float tmax;
             bool lh;
@@ -447,28 +455,29 @@ ND uint32_t shade_slot(const DScene& S, const WFArgs& A, uint32_t slot) {
 }
 
 // ---------------------------------------------------------------- shade
+// Slots are visited in index order (coalesced state rows); retired pixels are skipped.  Every
+// live slot has exactly one traced ray set to consume per iteration.
 template <int MAXL>
 __global__ __launch_bounds__(256) void k_wf_shade(DScene S, WFArgs A, uint32_t it) {
     const uint32_t cur = it & 1u, nxt = cur ^ 1u;
-    const uint32_t n = A.counts[2 + cur];
+    if (A.counts[4 + cur] == 0) return;
+    const uint32_t N = A.R.n_slots;
     const uint32_t gsize = gridDim.x * blockDim.x;
-    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gsize) {
-        const uint32_t qi = base + threadIdx.x;
-        uint32_t emit = 0, slot = 0;
-        if (qi < n) {
-            slot = A.sq[cur][qi];
-            emit = shade_slot<MAXL>(S, A, slot);
+    for (uint32_t base = blockIdx.x * blockDim.x; base < N; base += gsize) {
+        const uint32_t slot = base + threadIdx.x;
+        uint32_t emit = 0;
+        if (slot < N) {
+            const uint4 u = A.st.u[slot];
+            if (!(u.w & WF_DEAD)) emit = shade_slot<MAXL>(S, A, slot, u);
         }
-        const uint32_t nr = __popc(emit);
-        const uint32_t ri = wave_append(&A.counts[nxt], nr);
-        const uint32_t si = wave_append(&A.counts[2 + nxt], nr ? 1u : 0u);
-        if (nr) {
-            uint32_t* rq = A.rq[nxt] + ri;
-            if (emit & 1u) *rq++ = (slot << 2) | RK_EXT;
-            if (emit & 2u) *rq++ = (slot << 2) | RK_SH1;
-            if (emit & 4u) *rq++ = (slot << 2) | RK_SH2;
-            A.sq[nxt][si] = slot;
-        }
+        const uint32_t ri = wave_append(&A.counts[nxt], emit & 1u);
+        if (emit & 1u) A.rq_ext[nxt][ri] = slot;
+        const uint32_t nsh = ((emit >> 1) & 1u) + ((emit >> 2) & 1u);
+        uint32_t si = wave_append(&A.counts[2 + nxt], nsh);
+        if (emit & 2u) A.rq_sh[nxt][si++] = (slot << 2) | RK_SH1;
+        if (emit & 4u) A.rq_sh[nxt][si] = (slot << 2) | RK_SH2;
+        const uint32_t nlive = wave_sum(emit ? 1u : 0u);
+        if (__lane_id() == 0 && nlive) atomicAdd(&A.counts[4 + nxt], nlive);
     }
 }
 

@@ -204,8 +204,8 @@ int wf_layout(nart_ctx* ctx, uint32_t n, int maxl, WFArgs& w) {
     size_t o_c1 = take(N * 16), o_c2 = take(N * 16), o_bk = take(N * 16);
     size_t o_ro = take(3 * N * 16), o_rd = take(3 * N * 16), o_hit = take(N * 8), o_occ = take(3 * N);
     size_t o_ln = take(N * 4), o_lid = take((size_t)maxl * N * 4), o_leta = take((size_t)maxl * N * 4);
-    size_t o_rq0 = take(3 * N * 4), o_rq1 = take(3 * N * 4), o_sq0 = take(N * 4), o_sq1 = take(N * 4);
-    size_t o_cnt = take(16);
+    size_t o_re0 = take(N * 4), o_re1 = take(N * 4), o_rs0 = take(2 * N * 4), o_rs1 = take(2 * N * 4);
+    size_t o_cnt = take(6 * 4);
     if (off > ctx->cap_wf) {
         if (ctx->d_wf) hipFree(ctx->d_wf);
         ctx->d_wf = nullptr;
@@ -229,10 +229,10 @@ int wf_layout(nart_ctx* ctx, uint32_t n, int maxl, WFArgs& w) {
     T.ln = (uint32_t*)(b + o_ln);
     T.lid = (uint32_t*)(b + o_lid);
     T.leta = (float*)(b + o_leta);
-    w.rq[0] = (uint32_t*)(b + o_rq0);
-    w.rq[1] = (uint32_t*)(b + o_rq1);
-    w.sq[0] = (uint32_t*)(b + o_sq0);
-    w.sq[1] = (uint32_t*)(b + o_sq1);
+    w.rq_ext[0] = (uint32_t*)(b + o_re0);
+    w.rq_ext[1] = (uint32_t*)(b + o_re1);
+    w.rq_sh[0] = (uint32_t*)(b + o_rs0);
+    w.rq_sh[1] = (uint32_t*)(b + o_rs1);
     w.counts = (uint32_t*)(b + o_cnt);
     return NART_OK;
 }
@@ -263,7 +263,7 @@ int run_wavefront(nart_ctx* ctx, const RenderArgs& ra, hipStream_t st) {
         HIPCHK(hipHostMalloc((void**)&ctx->h_counts, 4 * sizeof(uint32_t), hipHostMallocDefault));
         for (auto& e : ctx->ev_chunk) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
-    HIPCHK(hipMemsetAsync(w.counts, 0, 4 * sizeof(uint32_t), st));
+    HIPCHK(hipMemsetAsync(w.counts, 0, 6 * sizeof(uint32_t), st));
     const uint32_t init_grid = std::min<uint32_t>((ra.n_slots + 255) / 256, 4096);
     hipLaunchKernelGGL(k_wf_init, dim3(init_grid), dim3(256), 0, st, ctx->scene, w);
     HIPCHK(hipGetLastError());
@@ -279,7 +279,7 @@ int run_wavefront(nart_ctx* ctx, const RenderArgs& ra, hipStream_t st) {
         }
         HIPCHK(hipGetLastError());
         // slots queued for iteration `it` (written by shade(it - 1))
-        HIPCHK(hipMemcpyAsync(&ctx->h_counts[chunk & 1], &w.counts[2 + (it & 1)], 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(&ctx->h_counts[chunk & 1], &w.counts[4 + (it & 1)], 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipEventRecord(ctx->ev_chunk[chunk & 1], st));
         if (chunk > 0) {
             HIPCHK(hipEventSynchronize(ctx->ev_chunk[(chunk - 1) & 1]));
