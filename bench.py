@@ -29,17 +29,21 @@ import torch  # noqa: E402
 
 import nart_amd  # noqa: E402
 from nart_amd import scenes  # noqa: E402
+from nart_amd.dist import BucketShard  # noqa: E402
 
 WIDTH, HEIGHT, SPP = 1920, 1080, 256
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md, chip-level parameters)
 
 
 def bytes_per_sample(c):
-    """Algorithmic bytes moved through the memory hierarchy per traced sample:
-    64 B per BVH2 node visit, 64 B per triangle record tested, 96 B winner Triangle record
-    per extension hit, 8 B image sample read + 16 B Li_alpha written per sample."""
+    """Algorithmic bytes per traced sample of the path-tracing kernel, SURVEY.md 8(d) minus the
+    splat term (the splat is its own kernel): per extension ray 64 B ray record + 32 B hit
+    record + 64 B winner attributes, per shadow ray 64 B ray + 4 B result, 64 B per BVH2 node
+    visit, 48 B per triangle test, 256 B path state per shaded hit, 40 B camera-ray generation
+    per sample."""
     n = max(1, c["traced_samples"])
-    return (64.0 * c["node_visits"] + 64.0 * c["tri_tests"] + 96.0 * c["rays_extend"]) / n + 24.0
+    return (160.0 * c["rays_extend"] + 68.0 * c["rays_shadow"] + 64.0 * c["node_visits"] + 48.0 * c["tri_tests"]
+            + 256.0 * c["bounces"]) / n + 40.0
 
 
 def cpu_baseline(scene, p):
@@ -104,33 +108,18 @@ def main():
     g = nart_amd.session_geometry(p)
     nb = g.n_buckets_x * g.n_buckets_y
     tpx = g.tile_size * g.tile_size
-    mine = np.arange(rank, nb, world, dtype=np.uint32)  # interleaved buckets: balanced cost per rank
-    per_rank = (nb + world - 1) // world
     gpu = nart_amd.HipRenderer(scene, device=local)
     stream = torch.cuda.current_stream()
     dev = torch.device("cuda", local)
-    tiles = torch.zeros((per_rank, tpx, 5), dtype=torch.float32, device=dev)
+    shard = BucketShard(nb, tpx, rank, world, dev)  # interleaved buckets, gather to rank 0
+    mine = shard.mine
     if rank == 0:
-        gathered = torch.zeros((world, per_rank, tpx, 5), dtype=torch.float32, device=dev)
-        by_id = torch.zeros((nb, tpx, 5), dtype=torch.float32, device=dev)
         image = torch.zeros((g.total_height, g.total_width, 5), dtype=torch.float32, device=dev)
-        order = torch.from_numpy(np.concatenate([np.arange(r, nb, world) for r in range(world)]).astype(np.int64)).to(dev)
-        slots = torch.from_numpy(np.concatenate([r * per_rank + np.arange(len(range(r, nb, world)))
-                                                 for r in range(world)]).astype(np.int64)).to(dev)
 
     def step(stats):
-        gpu.render_buckets_async(p, mine, tiles.data_ptr(), stream.cuda_stream, stats)
-        if dist:
-            import torch.distributed as td
-            if rank == 0:
-                td.gather(tiles, gather_list=list(gathered.unbind(0)), dst=0)
-            else:
-                td.gather(tiles, dst=0)
-        else:
-            gathered_view = tiles.unsqueeze(0)
+        gpu.render_buckets_async(p, mine, shard.tiles.data_ptr(), stream.cuda_stream, stats)
+        by_id = shard.gather()
         if rank == 0:
-            src = gathered.view(world * per_rank, tpx, 5) if dist else gathered_view.view(per_rank, tpx, 5)
-            by_id[order] = src[slots]
             gpu.combine_async(p, by_id.data_ptr(), image.data_ptr(), stream.cuda_stream)
 
     def barrier():
@@ -198,7 +187,8 @@ def main():
             "latin_ms_per_step": round(st.latin_ms / a.steps, 3),
             "image_finite": img_ok,
             "counters_per_sample": {k: round(counters[k] / max(1, counters["traced_samples"]), 3)
-                                    for k in ("rays_extend", "rays_shadow", "node_visits", "tri_tests")},
+                                    for k in ("rays_extend", "rays_shadow", "node_visits", "tri_tests",
+                                              "bounces")},
         }
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(scene, p)

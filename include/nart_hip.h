@@ -35,7 +35,8 @@ typedef struct nart_render_stats {
     uint32_t reserved;
     uint64_t samples;       /* camera samples counted in the metric (W*H*spp share)     */
     uint64_t traced_samples;/* samples actually traced (incl. extra rows, render.cpp:164) */
-    /* Counter pass only (nart_hip_set_counters(ctx,1)); zero otherwise. */
+    /* Counter pass only (nart_hip_set_counters(ctx,1)); zero otherwise.  bounces = extension
+     * hits shaded (BSDF + EstimateDirect + continuation). */
     uint64_t rays_extend, rays_shadow, node_visits, tri_tests, bounces;
     double latin_ms;        /* device time of the LatinSquare kernel                    */
 } nart_render_stats;

@@ -230,7 +230,7 @@ __global__ __launch_bounds__(256) void k_render(DScene S, RenderArgs A) {
             cur = ray;
             tmax = lightTMax;
             stage = ST_EXT;
-            if (COUNT) { ++n_ext; ++n_bounce; }
+            if (COUNT) ++n_ext;
         }
 
         float bt;
@@ -248,6 +248,7 @@ __global__ __launch_bounds__(256) void k_render(DScene S, RenderArgs A) {
                 new_sample = true;
                 continue;
             }
+            if (COUNT) ++n_bounce;  // shaded hit
             Isect is;
             fill_isect(S, cur, bg, is);
             BSDF bsdf;

@@ -174,7 +174,7 @@ __global__ __launch_bounds__(256) void k_wf_trace(DScene S, WFArgs A, uint32_t i
     const uint32_t gsize = gridDim.x * blockDim.x;
     const size_t N = A.R.n_slots;
     TraceCounters cnt = {0u, 0u};
-    uint32_t n_ext = 0, n_sh = 0;
+    uint32_t n_ext = 0, n_sh = 0, n_hit = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gsize) {
         const uint32_t tag = i < ne ? (A.rq_ext[cur][i] << 2) : A.rq_sh[cur][i - ne];
         const uint32_t slot = tag >> 2, kind = tag & 3u;
@@ -186,7 +186,10 @@ __global__ __launch_bounds__(256) void k_wf_trace(DScene S, WFArgs A, uint32_t i
         const bool hit = traverse<COUNT>(S, r, o.w, kind != RK_EXT, bt, bg, sc, stn, blockDim.x, cnt);
         if (kind == RK_EXT) {
             A.st.hit[slot] = make_uint2(__float_as_uint(bt), hit ? bg : NO_HIT);
-            if (COUNT) ++n_ext;
+            if (COUNT) {
+                ++n_ext;
+                n_hit += hit ? 1u : 0u;
+            }
         } else {
             A.st.occ[kind * N + slot] = hit ? 1 : 0;
             if (COUNT) ++n_sh;
@@ -194,12 +197,13 @@ __global__ __launch_bounds__(256) void k_wf_trace(DScene S, WFArgs A, uint32_t i
     }
     if (COUNT) {
         const uint32_t e = wave_sum(n_ext), sh = wave_sum(n_sh), nv = wave_sum(cnt.nodes), tt = wave_sum(cnt.tris);
+        const uint32_t hh = wave_sum(n_hit);
         if (__lane_id() == 0) {
             atomicAdd(&A.R.counters[0], (unsigned long long)e);
             atomicAdd(&A.R.counters[1], (unsigned long long)sh);
             atomicAdd(&A.R.counters[2], (unsigned long long)nv);
             atomicAdd(&A.R.counters[3], (unsigned long long)tt);
-            atomicAdd(&A.R.counters[4], (unsigned long long)e);
+            atomicAdd(&A.R.counters[4], (unsigned long long)hh);
         }
     }
 }

@@ -1,0 +1,47 @@
+"""Multi-GPU render: one process per GPU, buckets sharded across ranks, tiles gathered to rank 0.
+
+The reference renders the 16x16 buckets of a session with a tbb::task_group and sums their
+tiles into the image in bucket raster order (render.cpp:152-203).  Across ranks:
+  * rank r renders buckets r, r + N, r + 2N, ... (interleaved: the costly sphere region spreads
+    evenly over ranks, with no host work queue);
+  * each rank's tiles (tileSize^2 Pixels per bucket) are gathered to rank 0 with one
+    torch.distributed gather (RCCL over xGMI on GPUs, gloo in the CPU tests);
+  * rank 0 scatters them into bucket-id order and combines in bucket raster order, so the
+    image is bit-identical for any N.
+No other collective is on the data path.
+"""
+import numpy as np
+import torch
+
+
+class BucketShard:
+    """Bucket ownership and the tile gather for one rank of an N-rank render."""
+
+    def __init__(self, n_buckets, tile_pixels, rank, world, device):
+        self.nb, self.tpx, self.rank, self.world = n_buckets, tile_pixels, rank, world
+        self.mine = np.arange(rank, n_buckets, world, dtype=np.uint32)
+        self.per_rank = (n_buckets + world - 1) // world
+        self.tiles = torch.zeros((self.per_rank, tile_pixels, 5), dtype=torch.float32, device=device)
+        self.gathered = self.by_id = None
+        if rank == 0:
+            self.gathered = torch.zeros((world, self.per_rank, tile_pixels, 5), dtype=torch.float32, device=device)
+            self.by_id = torch.zeros((n_buckets, tile_pixels, 5), dtype=torch.float32, device=device)
+            owned = [np.arange(r, n_buckets, world) for r in range(world)]
+            self.order = torch.from_numpy(np.concatenate(owned).astype(np.int64)).to(device)
+            self.slots = torch.from_numpy(np.concatenate(
+                [r * self.per_rank + np.arange(len(o)) for r, o in enumerate(owned)]).astype(np.int64)).to(device)
+
+    def gather(self):
+        """Collective: rank 0 returns the (n_buckets, tileSize^2, 5) tiles in bucket-id order."""
+        if self.world > 1:
+            import torch.distributed as td
+            if self.rank == 0:
+                td.gather(self.tiles, gather_list=list(self.gathered.unbind(0)), dst=0)
+            else:
+                td.gather(self.tiles, dst=0)
+                return None
+            src = self.gathered.view(self.world * self.per_rank, self.tpx, 5)
+        else:
+            src = self.tiles
+        self.by_id[self.order] = src[self.slots]
+        return self.by_id

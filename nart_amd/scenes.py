@@ -38,7 +38,12 @@ def _write_geo(path, kinds, ints, floats):
 
 
 def write_geo(path, faces, verts, normals, face_normals, uvs=None, face_uvs=None):
-    """Write a .geo mesh (LoadMeshFromFile layout, scene.cpp:91-223)."""
+    """Write a .geo mesh (LoadMeshFromFile layout, scene.cpp:91-223).  The reader sizes each
+    coordinate array by the largest index referencing it, so arrays are cut to that length."""
+    verts = verts[:max(i for f in faces for i in f) + 1]
+    normals = normals[:max(i for f in face_normals for i in f) + 1]
+    if uvs is not None:
+        uvs = uvs[:max(i for f in face_uvs for i in f) + 1]
     toks = [str(len(faces))] + [str(len(f)) for f in faces]
     toks += [str(i) for f in faces for i in f]
     toks += [_fmt(c) for v in verts for c in v]
@@ -123,6 +128,117 @@ def cornell(directory=None, width=1920, height=1080, spp=64):
                     "transform": [1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 1.98, 0, 0, 0, 1]}],
     }
     path = os.path.join(d, "cornell.json")
+    with open(path, "w") as f:
+        json.dump(scene, f, indent=1)
+    return path
+
+
+def write_texture(path, rgba, compression=3):
+    """Write an (H, W, 4) float array as a half-RGBA EXR through the drop-in's own writer
+    (WriteImageToEXR layout: a Pixel framebuffer with a 1-pixel border and unit weights)."""
+    from . import api
+    rgba = np.asarray(rgba, np.float32)
+    h, w = rgba.shape[:2]
+    p = api.default_params()
+    p.image_width, p.image_height, p.filter_width = w, h, 1.0
+    img = np.zeros((h + 2, w + 2, 5), np.float32)
+    img[1:h + 1, 1:w + 1, :4] = rgba
+    img[..., 4] = 1.0
+    api.write_exr(path, p, img, compression)
+
+
+def _uv_sphere(center, radius, n_lat=12, n_lon=24):
+    """Lat-long sphere with per-vertex normals and UVs (quads, triangle caps)."""
+    c = np.asarray(center, np.float64)
+    verts, normals, uvs = [], [], []
+    for j in range(n_lat + 1):
+        th = np.pi * j / n_lat
+        for i in range(n_lon + 1):
+            ph = 2 * np.pi * i / n_lon
+            n = np.array([np.sin(th) * np.cos(ph), np.sin(th) * np.sin(ph), np.cos(th)])
+            verts.append(tuple(c + radius * n))
+            normals.append(tuple(n))
+            uvs.append((i / n_lon, 1 - j / n_lat))
+    faces = []
+    for j in range(n_lat):
+        for i in range(n_lon):
+            a, b = j * (n_lon + 1) + i, (j + 1) * (n_lon + 1) + i
+            if j == 0:
+                faces.append([a, b, b + 1])
+            elif j == n_lat - 1:
+                faces.append([a, b, a + 1])
+            else:
+                faces.append([a, b, b + 1, a + 1])
+    return faces, verts, normals, faces, uvs, faces
+
+
+def _uv_grid(origin, u, v, n, res):
+    faces, verts, normals, fn = _grid_quad(origin, u, v, n, res)
+    uvs = [(i / res, j / res) for j in range(res + 1) for i in range(res + 1)]
+    return faces, verts, normals, fn, uvs, faces
+
+
+def materials(directory=None, width=320, height=240, spp=16):
+    """Every material type, textured / roughness-textured / normal-mapped patterns, a ring and
+    a disk light and nested dielectric priorities -- the device paths glassSphere and the
+    Cornell box leave untouched.  Textures are generated (no RNG) and written as ZIP EXRs."""
+    d = directory or tempfile.mkdtemp(prefix="nart_materials_")
+    os.makedirs(d, exist_ok=True)
+    n = 64
+    yy, xx = np.mgrid[0:n, 0:n].astype(np.float32) / (n - 1)
+    check = ((np.floor(xx * 8) + np.floor(yy * 8)) % 2).astype(np.float32)
+    albedo = np.stack([0.2 + 0.6 * xx, 0.15 + 0.5 * check, 0.7 - 0.5 * yy, np.ones_like(xx)], -1)
+    bump = np.stack([0.5 + 0.35 * np.sin(xx * 12.0), 0.5 + 0.35 * np.cos(yy * 9.0),
+                     np.full_like(xx, 0.9), np.ones_like(xx)], -1)
+    rough = np.stack([0.05 + 0.6 * xx, 0.05 + 0.6 * xx, 0.05 + 0.6 * xx, np.ones_like(xx)], -1)
+    tex = {}
+    for name, arr in (("albedo", albedo), ("bump", bump), ("rough", rough)):
+        tex[name] = os.path.join(d, name + ".exr")
+        write_texture(tex[name], arr)
+    geo = {}
+    geo["ground"] = _uv_grid((-3, -3, 0), (6, 0, 0), (0, 6, 0), (0, 0, 1), 6)
+    geo["back"] = _uv_grid((-3, 2.5, 0), (6, 0, 0), (0, 0, 4), (0, -1, 0), 4)
+    geo["glossy"] = _uv_sphere((-1.4, 0.4, 0.6), 0.6)
+    geo["mirror"] = _uv_sphere((0.0, 0.9, 0.6), 0.6)
+    geo["plastic"] = _uv_sphere((1.4, 0.4, 0.6), 0.6)
+    geo["glass"] = _uv_sphere((0.2, -0.8, 0.45), 0.45)
+    geo["inner"] = _uv_sphere((0.2, -0.8, 0.45), 0.25, 8, 16)
+    for k, g in geo.items():
+        write_geo(os.path.join(d, k + ".geo"), *g)
+    T = lambda p: {"type": "texture", "filePath": p}  # noqa: E731
+    meshes = [
+        ("ground", {"type": "plastic", "rho_d": T(tex["albedo"]), "rho_s": [0.9, 0.9, 0.9], "eta": 1.5,
+                    "roughness": 0.2, "normal": T(tex["bump"])}, None),
+        ("back", {"type": "lambert", "rho_d": T(tex["albedo"]), "normal": T(tex["bump"])}, None),
+        ("glossy", {"type": "glossy", "rho_s": [0.95, 0.64, 0.54], "eta": 1.8, "roughness": T(tex["rough"])}, None),
+        ("mirror", {"type": "specular", "rho_s": [0.9, 0.9, 0.9], "eta": 8192}, None),
+        ("plastic", {"type": "plastic", "rho_d": [0.1, 0.3, 0.6], "rho_s": [1, 1, 1], "eta": 1.5,
+                     "roughness": 0.0}, None),
+        ("glass", {"type": "glass", "rho_s": [1, 1, 1], "tau": [0.9, 0.95, 1.0], "eta": 1.5,
+                   "roughness": 0.15}, 2),
+        ("inner", {"type": "glass", "rho_s": [1, 1, 1], "tau": [1.0, 0.6, 0.6], "eta": 1.33,
+                   "roughness": 0.0}, 3),
+    ]
+    jm = []
+    for name, mat, prio in meshes:
+        e = {"filePath": os.path.join(d, name + ".geo"), "material": mat}
+        if prio is not None:
+            e["priority"] = prio
+        jm.append(e)
+    scene = {
+        "renderSessions": [{"imageWidth": width, "imageHeight": height, "bucketSize": 16, "spp": spp,
+                            "bounces": 12, "filterWidth": 1.5, "rougheningFactor": 0.3}],
+        "camera": {"fov": 24.0, "transform": [1, 0, 0, 0, 0, 0.2588190, -0.9659258, -6.2, 0, 0.9659258, 0.2588190, 2.0,
+                                              0, 0, 0, 1]},
+        "meshes": jm,
+        "lights": [
+            {"type": "ring", "radius": 0.8, "innerRadius": 0.4, "Le": [1.0, 0.9, 0.8], "intensity": 30.0,
+             "transform": [1, 0, 0, 0.5, 0, 1, 0, -0.5, 0, 0, 1, 3.2, 0, 0, 0, 1]},
+            {"type": "disk", "radius": 0.3, "Le": [0.6, 0.7, 1.0], "intensity": 60.0,
+             "transform": [1, 0, 0, -2.0, 0, 0, 1, 1.5, 0, -1, 0, 1.2, 0, 0, 0, 1]},
+        ],
+    }
+    path = os.path.join(d, "materials.json")
     with open(path, "w") as f:
         json.dump(scene, f, indent=1)
     return path

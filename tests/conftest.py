@@ -37,6 +37,13 @@ def cornell_scene(built, tmp_path_factory):
 
 
 @pytest.fixture(scope="session")
+def materials_scene(built, tmp_path_factory):
+    import nart_amd
+    from nart_amd import scenes
+    return nart_amd.Scene(scenes.materials(str(tmp_path_factory.mktemp("materials"))))
+
+
+@pytest.fixture(scope="session")
 def gpu(built):
     import torch
     assert torch.cuda.is_available(), "GPU tests need a visible MI355X"

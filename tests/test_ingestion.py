@@ -147,3 +147,26 @@ def test_reads_reference_style_texture(tmp_path):
     nart_amd.write_exr(path, p, img, 3)
     tex = nart_amd.read_exr(path)
     assert tex.shape == (40, 64, 4) and tex[..., 3].min() == 1.0
+
+
+def test_texture_writer_reader_roundtrip(built, tmp_path):
+    """scenes.write_texture (WriteImageToEXR layout, ZIP) read back by the RgbaInputFile path."""
+    import numpy as np
+    import nart_amd
+    from nart_amd import scenes
+    rng = np.random.default_rng(3)
+    a = rng.random((37, 53, 4)).astype(np.float32) * 4
+    for comp in (0, 3):
+        path = str(tmp_path / ("t%d.exr" % comp))
+        scenes.write_texture(path, a, comp)
+        b = nart_amd.read_exr(path)
+        assert b.shape == a.shape
+        assert np.array_equal(b, a.astype(np.float16).astype(np.float32))
+
+
+def test_materials_scene_ingests(built, tmp_path):
+    import nart_amd
+    from nart_amd import scenes
+    sc = nart_amd.Scene(scenes.materials(str(tmp_path)))
+    c = sc.counts()
+    assert c["materials"] == 7 and c["lights"] == 2 and c["textures"] >= 3
