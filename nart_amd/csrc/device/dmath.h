@@ -148,6 +148,136 @@ ND uint32_t xorshift(uint32_t y) {
     y ^= (y << 5);
     return y;
 }
+// ---------------------------------------------------------------- glibc 2.35 acosf / atanf / atan2f
+// sysdeps/ieee754/flt-32/{e_acosf,s_atanf,e_atan2f}.c: the fdlibm single-precision algorithms,
+// plain float arithmetic (no FMA contraction on x86-64).  Restated so the environment light's
+// lat-long mapping (environmentlight.cpp:9-28) rounds exactly as the reference's libm does;
+// tests/native/libm_port_check.cpp compares them with this host's glibc.
+NHD float fbits(uint32_t u) { return __builtin_bit_cast(float, u); }
+NHD uint32_t ubits(float f) { return __builtin_bit_cast(uint32_t, f); }
+
+NHD float acosf_rpoly(float z) {
+    const float pS0 = fbits(0x3e2aaaabu), pS1 = fbits(0xbea6b090u), pS2 = fbits(0x3e4e0aa8u),
+                pS3 = fbits(0xbd241146u), pS4 = fbits(0x3a4f7f04u), pS5 = fbits(0x3811ef08u),
+                qS1 = fbits(0xc019d139u), qS2 = fbits(0x4001572du), qS3 = fbits(0xbf303361u),
+                qS4 = fbits(0x3d9dc62eu);
+    float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    return p / q;
+}
+NHD float glibc_acosf(float x) {
+    const float pi = fbits(0x40490fdau), pio2_hi = fbits(0x3fc90fdau), pio2_lo = fbits(0x33a22168u);
+    const int32_t hx = (int32_t)ubits(x);
+    const int32_t ix = hx & 0x7fffffff;
+    if (ix == 0x3f800000) return hx > 0 ? 0.0f : pi + 2.0f * pio2_lo;
+    if (ix > 0x3f800000) return (x - x) / (x - x);
+    if (ix < 0x3f000000) {  // |x| < 0.5
+        if (ix <= 0x32800000) return pio2_hi + pio2_lo;
+        float z = x * x;
+        float r = acosf_rpoly(z);
+        return pio2_hi - (x - (pio2_lo - x * r));
+    }
+    if (hx < 0) {  // x < -0.5
+        float z = (1.0f + x) * 0.5f;
+        float r = acosf_rpoly(z);
+        float s = sqrtf(z);
+        float w = r * s - pio2_lo;
+        return pi - 2.0f * (s + w);
+    }
+    float z = (1.0f - x) * 0.5f;  // x > 0.5
+    float s = sqrtf(z);
+    float df = fbits(ubits(s) & 0xfffff000u);
+    float c = (z - df * df) / (s + df);
+    float r = acosf_rpoly(z);
+    float w = r * s + c;
+    return 2.0f * (df + w);
+}
+
+NHD float glibc_atanf(float x) {
+    const float atanhi[4] = {fbits(0x3eed6338u), fbits(0x3f490fdau), fbits(0x3f7b985eu), fbits(0x3fc90fdau)};
+    const float atanlo[4] = {fbits(0x31ac3769u), fbits(0x33222168u), fbits(0x33140fb4u), fbits(0x33a22168u)};
+    const float aT0 = fbits(0x3eaaaaabu), aT1 = fbits(0xbe4ccccdu), aT2 = fbits(0x3e124925u),
+                aT3 = fbits(0xbde38e38u), aT4 = fbits(0x3dba2e6eu), aT5 = fbits(0xbd9d8795u),
+                aT6 = fbits(0x3d886b35u), aT7 = fbits(0xbd6ef16bu), aT8 = fbits(0x3d4bda59u),
+                aT9 = fbits(0xbd15a221u), aT10 = fbits(0x3c8569d7u);
+    const int32_t hx = (int32_t)ubits(x);
+    const int32_t ix = hx & 0x7fffffff;
+    int id;
+    if (ix >= 0x4c000000) {  // |x| >= 2^25
+        if (ix > 0x7f800000) return x + x;
+        return hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
+    }
+    if (ix < 0x3ee00000) {  // |x| < 0.4375
+        if (ix < 0x31000000) return x;  // |x| < 2^-29
+        id = -1;
+    } else {
+        x = fabsf(x);
+        if (ix < 0x3f980000) {      // |x| < 1.1875
+            if (ix < 0x3f300000) {  // 7/16 <= |x| < 11/16
+                id = 0;
+                x = (2.0f * x - 1.0f) / (2.0f + x);
+            } else {
+                id = 1;
+                x = (x - 1.0f) / (x + 1.0f);
+            }
+        } else {
+            if (ix < 0x401c0000) {  // |x| < 2.4375
+                id = 2;
+                x = (x - 1.5f) / (1.0f + 1.5f * x);
+            } else {
+                id = 3;
+                x = -1.0f / x;
+            }
+        }
+    }
+    float z = x * x;
+    float w = z * z;
+    float s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+    float s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+    if (id < 0) return x - x * (s1 + s2);
+    float hi = id == 0 ? atanhi[0] : id == 1 ? atanhi[1] : id == 2 ? atanhi[2] : atanhi[3];
+    float lo = id == 0 ? atanlo[0] : id == 1 ? atanlo[1] : id == 2 ? atanlo[2] : atanlo[3];
+    z = hi - ((x * (s1 + s2) - lo) - x);
+    return hx < 0 ? -z : z;
+}
+
+NHD float glibc_atan2f(float y, float x) {
+    const float tiny = 1.0e-30f, pi_o_4 = fbits(0x3f490fdbu), pi_o_2 = fbits(0x3fc90fdbu),
+                pi = fbits(0x40490fdbu), pi_lo = fbits(0xb3bbbd2eu);
+    const int32_t hx = (int32_t)ubits(x), ix = hx & 0x7fffffff;
+    const int32_t hy = (int32_t)ubits(y), iy = hy & 0x7fffffff;
+    if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;
+    if (hx == 0x3f800000) return glibc_atanf(y);
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+    if (iy == 0) {
+        if (m <= 1) return y;
+        return m == 2 ? pi + tiny : -pi - tiny;
+    }
+    if (ix == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    if (ix == 0x7f800000) {
+        if (iy == 0x7f800000) {
+            if (m == 0) return pi_o_4 + tiny;
+            if (m == 1) return -pi_o_4 - tiny;
+            if (m == 2) return 3.0f * pi_o_4 + tiny;
+            return -3.0f * pi_o_4 - tiny;
+        }
+        if (m == 0) return 0.0f;
+        if (m == 1) return -0.0f;
+        if (m == 2) return pi + tiny;
+        return -pi - tiny;
+    }
+    if (iy == 0x7f800000) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    const int32_t k = (iy - ix) >> 23;
+    float z;
+    if (k > 60) z = pi_o_2 + 0.5f * pi_lo;
+    else if (hx < 0 && k < -60) z = 0.0f;
+    else z = glibc_atanf(fabsf(y / x));
+    if (m == 0) return z;
+    if (m == 1) return fbits(ubits(z) ^ 0x80000000u);
+    if (m == 2) return pi - (z - pi_lo);
+    return (z - pi_lo) - pi;
+}
+
 ND float rng_float(uint32_t& y) {
     y = xorshift(y);
     float f = (float)(uint32_t)(y * 0x9E3779BBu) * 2.3283064365386963e-10f;

@@ -1,13 +1,34 @@
-// Light::Li / Light::Sample_Li dispatch for the device path (disk and ring area lights).
-// The environment light (environmentlight.cpp:9-79) needs glibc-exact acosf/atan2f ports;
-// until those land, nart_hip_create rejects scenes with an environment light
-// (NART_E_UNSUPPORTED) instead of rendering them with a different libm.
+// Light::Li / Light::Sample_Li dispatch for the device path: disk and ring area lights and the
+// lat-long environment light (environmentlight.cpp:9-79) with its Piecewise2DDistribution
+// importance sampling (texturepattern.cpp:3-170).  acosf / atan2f / sinf / cosf are the glibc
+// restatements of dmath.h, so the mapping rounds exactly as the reference's libm.
 #pragma once
 
 namespace nd {
 
-// Light::Li (disklight.cpp:12-23, ringlight.cpp:117-128)
+#define ENV_TMAX 2139095040.0f  // (float)0x7f7fffff (environmentlight.cpp:26, 59)
+
+// TexturePattern::Pdf / ConstantPattern::Pdf of the env light's Le (texturepattern.cpp:160-170)
+ND float env_ptn_pdf(const DScene& S, const DLight& L, f2 st) {
+    if (L.Le.type == NART_PTN_CONSTANT || L.env < 0) return 1.f;
+    return env_pdf(S.envs[L.env], F2(gmin(st.x, 0.9999f), gmin(st.y, 0.9999f)));
+}
+
+// Light::Li (disklight.cpp:12-23, ringlight.cpp:117-128, environmentlight.cpp:9-28)
 ND f3 light_li(const DScene& S, const DLight& L, f3 p, f3 wi, float* pdf, float& tMax) {
+    if (L.type == NART_LIGHT_ENVIRONMENT) {
+        const float theta = glibc_acosf(wi.z);
+        float phi = glibc_atan2f(wi.y, wi.x) + ND_PI;
+        if (phi > ND_TWO_PI) phi -= ND_TWO_PI;
+        if (phi < 0.f) phi += ND_TWO_PI;
+        const f2 est = F2(1.f - (phi * ND_ONE_OVER_TWO_PI), 1.f - (theta * ND_ONE_OVER_PI));
+        if (pdf) {
+            *pdf = env_ptn_pdf(S, L, est);
+            *pdf *= ND_ONE_OVER_PI * 0.25f / gabs(glibc_sinf(theta));
+        }
+        tMax = ENV_TMAX;
+        return muls(ptn_value(S, L.Le, est), L.intensity);
+    }
     f2 st = F2(0.f, 0.f);
     float lp = area_pdf(L, p, wi, st, tMax);
     if (lp > 0.f) {
@@ -19,6 +40,30 @@ ND f3 light_li(const DScene& S, const DLight& L, f3 p, f3 wi, float* pdf, float&
 
 // Light::Sample_Li (disklight.cpp:25-60, ringlight.cpp:130-168)
 ND f3 light_sample_li(const DScene& S, const DLight& L, f3 p, f3& wi, f2 sample, float& pdf, float& tMax) {
+    if (L.type == NART_LIGHT_ENVIRONMENT) {
+        // Pattern::Sample (constantpattern.cpp:3-14, texturepattern.cpp:130-158)
+        f2 ps = sample;
+        f3 Lv;
+        if (L.Le.type == NART_PTN_CONSTANT) {
+            pdf = 1.f;
+            Lv = F3(L.Le.v[0], L.Le.v[1], L.Le.v[2]);
+        } else {
+            if (L.env < 0) pdf = 1.f;
+            else ps = env_sample(S.envs[L.env], sample, pdf);  // leaves pdf as is on a zero row
+            Lv = tex_fetch(S, L.Le.tex, ps.x, ps.y, L.Le.rough);
+        }
+        Lv = muls(Lv, L.intensity);
+        const float theta = (1.f - ps.y) * ND_PI;
+        float phi = (1.f - ps.x) * 2.f * ND_PI;
+        phi += ND_PI;
+        if (phi > ND_TWO_PI) phi -= ND_TWO_PI;
+        if (phi < 0.f) phi += ND_TWO_PI;
+        const float st = glibc_sinf(theta);
+        wi = F3(glibc_cosf(phi) * st, glibc_sinf(phi) * st, glibc_cosf(theta));
+        pdf *= ND_ONE_OVER_PI * 0.25f / gabs(st);
+        tMax = ENV_TMAX;
+        return Lv;
+    }
     f4 ds;
     if (L.type == NART_LIGHT_RING) {
         f2 r = uniform_sample_ring(sample, pdf, L.inner_ratio);

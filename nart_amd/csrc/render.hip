@@ -33,6 +33,8 @@ struct nart_ctx {
     void* d_lights = nullptr;
     void* d_texs = nullptr;
     void* d_tex_pool = nullptr;
+    void* d_envs = nullptr;
+    std::vector<void*> env_bufs;  // Piecewise2DDistribution tables
     // work buffers
     size_t cap_slot_bytes = 0, cap_misc = 0;
     uint32_t* d_slot_xy = nullptr;
@@ -117,6 +119,66 @@ DLight dlight(const nart_light& L) {
     d.inner_ratio = L.inner_radius / L.radius;
     d.env = -1;
     return d;
+}
+
+// Piecewise2DDistribution of an environment texture (texturepattern.cpp:3-70): marginal pdf of
+// the rows (top row last), conditional pdf per row, and their CDFs, with the reference's float
+// operation order.  Built on the host once per context.
+int build_env(nart_ctx* ctx, const nart_texture& t, DEnvDist& d) {
+    const uint32_t W = t.width, H = t.height;
+    std::vector<float> mpdf(H), cpdf((size_t)W * H), mcdf(H + 1), ccdf((size_t)W * H + H);
+    auto texel = [&](uint32_t row, uint32_t i) {  // |r| + |g| + |b| of the flipped row
+        const uint16_t* q = t.rgba + ((size_t)(H - row - 1) * W + i) * 4;
+        return std::fabs(nart_half_to_float(q[0])) + std::fabs(nart_half_to_float(q[1])) +
+               std::fabs(nart_half_to_float(q[2]));
+    };
+    const float invW = 1.f / (float)W, invH = 1.f / (float)H;
+    float fInt = 0.f;
+    for (uint32_t j = 0; j < H; ++j) {
+        mpdf[j] = 0.f;
+        for (uint32_t i = 0; i < W; ++i) mpdf[j] += texel(j, i);
+        mpdf[j] *= invW;
+        fInt += mpdf[j];
+    }
+    fInt *= invH;
+    for (uint32_t j = 0; j < H; ++j) {
+        if (mpdf[j] != 0.f) {
+            for (uint32_t i = 0; i < W; ++i) {
+                cpdf[(size_t)j * W + i] = texel(j, i);
+                cpdf[(size_t)j * W + i] /= mpdf[j];
+            }
+        } else {
+            for (uint32_t i = 0; i < W; ++i) cpdf[(size_t)j * W + i] = 1.f;
+        }
+    }
+    const float invFInt = 1.f / fInt;
+    for (uint32_t j = 0; j < H; ++j) mpdf[j] *= invFInt;
+    mcdf[0] = 0.f;
+    mcdf[H] = 1.f;
+    for (uint32_t i = 1; i < H; ++i) mcdf[i] = mcdf[i - 1] + (mpdf[i - 1] * invH);
+    for (uint32_t i = 0; i < H; ++i) {
+        ccdf[(size_t)i * (W + 1)] = 0.f;
+        ccdf[(size_t)i * (W + 1) + W] = 1.f;
+    }
+    for (uint32_t j = 0; j < H; ++j)
+        for (uint32_t i = 1; i < W; ++i)
+            ccdf[(size_t)j * (W + 1) + i] = ccdf[(size_t)j * (W + 1) + i - 1] + (cpdf[(size_t)j * W + i - 1] * invW);
+    void* bufs[4] = {nullptr, nullptr, nullptr, nullptr};
+    const std::vector<float>* src[4] = {&mpdf, &cpdf, &mcdf, &ccdf};
+    for (int k = 0; k < 4; ++k) {
+        int rc = upload(ctx, bufs[k], src[k]->data(), src[k]->size());
+        if (bufs[k]) ctx->env_bufs.push_back(bufs[k]);
+        if (rc) return rc;
+    }
+    d.w = W;
+    d.h = H;
+    d.invW = invW;
+    d.invH = invH;
+    d.mpdf = (const float*)bufs[0];
+    d.cpdf = (const float*)bufs[1];
+    d.mcdf = (const float*)bufs[2];
+    d.ccdf = (const float*)bufs[3];
+    return NART_OK;
 }
 
 int check_params(nart_ctx* ctx, const nart_render_params* p) {
@@ -474,12 +536,10 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     if (hipFuncSetAttribute((const void*)k_latin_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
         hipSuccess)
         return bail(NART_E_HIP);
-    for (uint32_t l = 0; l < blob->num_lights; ++l)
-        if (blob->lights[l].type == NART_LIGHT_ENVIRONMENT) {
-            ctx->err = "environment lights are not supported on the device yet";
-            return bail(NART_E_UNSUPPORTED);
-        }
-    if (blob->medium.present) return bail(NART_E_UNSUPPORTED);
+    if (blob->medium.present) {
+        ctx->err = "volume integrator / camera medium not implemented on the device yet";
+        return bail(NART_E_UNSUPPORTED);
+    }
     // reference octree visibility (Q14) + device BVH
     std::vector<uint8_t> mask;
     bool root_leaf = false;
@@ -524,7 +584,18 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     }
     if ((rc = upload(ctx, ctx->d_mats, mats.data(), mats.size()))) return bail(rc);
     std::vector<DLight> lights;
-    for (uint32_t l = 0; l < blob->num_lights; ++l) lights.push_back(dlight(blob->lights[l]));
+    std::vector<DEnvDist> envs;
+    for (uint32_t l = 0; l < blob->num_lights; ++l) {
+        lights.push_back(dlight(blob->lights[l]));
+        const nart_light& L = blob->lights[l];
+        if (L.type == NART_LIGHT_ENVIRONMENT && L.Le.type == NART_PTN_TEXTURE) {
+            DEnvDist d;
+            if ((rc = build_env(ctx, blob->textures[L.Le.texture], d))) return bail(rc);
+            lights.back().env = (int32_t)envs.size();
+            envs.push_back(d);
+        }
+    }
+    if ((rc = upload(ctx, ctx->d_envs, envs.data(), envs.size()))) return bail(rc);
     if ((rc = upload(ctx, ctx->d_lights, lights.data(), lights.size()))) return bail(rc);
     std::vector<DTexture> texs(blob->num_textures);
     size_t pool = 0;
@@ -551,7 +622,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     S.lights = (const DLight*)ctx->d_lights;
     S.texs = (const DTexture*)ctx->d_texs;
     S.tex_pool = (const uint16_t*)ctx->d_tex_pool;
-    S.envs = nullptr;
+    S.envs = (const DEnvDist*)ctx->d_envs;
     S.num_lights = blob->num_lights;
     S.num_tris = blob->num_triangles;
     S.root = bvh.root_code;
@@ -568,9 +639,10 @@ void nart_hip_destroy(nart_ctx* ctx) {
     hipSetDevice(ctx->device);
     void* bufs[] = {ctx->d_nodes, ctx->d_tri_isect, ctx->d_tris, ctx->d_tri_mesh, ctx->d_meshes, ctx->d_mats,
                     ctx->d_lights, ctx->d_texs, ctx->d_tex_pool, ctx->d_slot_xy, ctx->d_rng, ctx->d_samples,
-                    ctx->d_L, ctx->d_bucket_ids, ctx->d_bucket_base, ctx->d_table, ctx->d_counters, ctx->d_wf};
+                    ctx->d_L, ctx->d_bucket_ids, ctx->d_bucket_base, ctx->d_table, ctx->d_counters, ctx->d_wf, ctx->d_envs};
     for (void* b : bufs)
         if (b) hipFree(b);
+    for (void* b : ctx->env_bufs) hipFree(b);
     if (ctx->events)
         for (auto& e : ctx->ev) hipEventDestroy(e);
     if (ctx->h_counts) {

@@ -242,3 +242,59 @@ def materials(directory=None, width=320, height=240, spp=16):
     with open(path, "w") as f:
         json.dump(scene, f, indent=1)
     return path
+
+
+def sky_texture(width=128, height=64, sun=(0.3, 0.35), sun_size=0.035, sun_power=60.0):
+    """Equirect sky (row 0 = zenith): blue-to-white gradient, dark ground, Gaussian sun.  Fixed
+    formula, no RNG."""
+    v, u = np.mgrid[0:height, 0:width].astype(np.float32)
+    u, v = (u + 0.5) / width, (v + 0.5) / height
+    up = np.clip(1.0 - 2.0 * v, 0.0, 1.0)
+    sky = np.stack([0.55 + 0.3 * (1 - up), 0.7 + 0.2 * (1 - up), np.full_like(up, 1.0)], -1) * (v < 0.5)[..., None]
+    ground = np.stack([0.18, 0.15, 0.12]) * np.ones_like(u)[..., None] * (v >= 0.5)[..., None]
+    d2 = (u - sun[0]) ** 2 + ((v - sun[1]) * 0.5) ** 2
+    s = sun_power * np.exp(-d2 / (2 * sun_size ** 2))
+    rgb = sky + ground + np.stack([s, 0.9 * s, 0.75 * s], -1)
+    return np.concatenate([rgb, np.ones_like(u)[..., None]], -1).astype(np.float32)
+
+
+def environment(directory=None, width=320, height=180, spp=16, textured_env=True):
+    """C4-style scene: a textured, normal-mapped plastic mesh, a rough glass sphere and a
+    textured Lambert ground lit only by an importance-sampled environment light
+    (environmentlight.cpp, Piecewise2DDistribution) built from sky_texture()."""
+    d = directory or tempfile.mkdtemp(prefix="nart_env_")
+    os.makedirs(d, exist_ok=True)
+    n = 64
+    yy, xx = np.mgrid[0:n, 0:n].astype(np.float32) / (n - 1)
+    check = ((np.floor(xx * 6) + np.floor(yy * 6)) % 2).astype(np.float32)
+    albedo = np.stack([0.25 + 0.5 * check, 0.3 + 0.4 * xx, 0.6 - 0.4 * yy, np.ones_like(xx)], -1)
+    bump = np.stack([0.5 + 0.3 * np.sin(xx * 20.0), 0.5 + 0.3 * np.sin(yy * 17.0), np.full_like(xx, 0.95),
+                     np.ones_like(xx)], -1)
+    paths = {k: os.path.join(d, k + ".exr") for k in ("albedo", "bump", "sky")}
+    write_texture(paths["albedo"], albedo)
+    write_texture(paths["bump"], bump)
+    write_texture(paths["sky"], sky_texture())
+    write_geo(os.path.join(d, "ground.geo"), *_uv_grid((-4, -4, 0), (8, 0, 0), (0, 8, 0), (0, 0, 1), 4))
+    write_geo(os.path.join(d, "ball.geo"), *_uv_sphere((-0.7, 0.2, 0.8), 0.8, 16, 32))
+    write_geo(os.path.join(d, "glass.geo"), *_uv_sphere((1.0, -0.4, 0.5), 0.5))
+    T = lambda p: {"type": "texture", "filePath": p}  # noqa: E731
+    scene = {
+        "renderSessions": [{"imageWidth": width, "imageHeight": height, "bucketSize": 16, "spp": spp,
+                            "bounces": 8, "filterWidth": 2, "rougheningFactor": 0.2}],
+        "camera": {"fov": 22.0, "transform": [1, 0, 0, 0, 0, 0.2588190, -0.9659258, -6.0, 0, 0.9659258, 0.2588190,
+                                              2.0, 0, 0, 0, 1]},
+        "meshes": [
+            {"filePath": os.path.join(d, "ground.geo"), "material": {"type": "lambert", "rho_d": T(paths["albedo"])}},
+            {"filePath": os.path.join(d, "ball.geo"),
+             "material": {"type": "plastic", "rho_d": T(paths["albedo"]), "rho_s": [1, 1, 1], "eta": 1.5,
+                          "roughness": 0.25, "normal": T(paths["bump"])}},
+            {"filePath": os.path.join(d, "glass.geo"),
+             "material": {"type": "glass", "rho_s": [1, 1, 1], "tau": [1, 1, 1], "eta": 1.5, "roughness": 0.1}},
+        ],
+        "lights": [{"type": "environment", "Le": T(paths["sky"]) if textured_env else [0.8, 0.85, 1.0],
+                    "intensity": 1.5}],
+    }
+    path = os.path.join(d, "environment.json")
+    with open(path, "w") as f:
+        json.dump(scene, f, indent=1)
+    return path

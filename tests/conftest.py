@@ -44,6 +44,20 @@ def materials_scene(built, tmp_path_factory):
 
 
 @pytest.fixture(scope="session")
+def env_scene(built, tmp_path_factory):
+    import nart_amd
+    from nart_amd import scenes
+    return nart_amd.Scene(scenes.environment(str(tmp_path_factory.mktemp("env"))))
+
+
+@pytest.fixture(scope="session")
+def env_const_scene(built, tmp_path_factory):
+    import nart_amd
+    from nart_amd import scenes
+    return nart_amd.Scene(scenes.environment(str(tmp_path_factory.mktemp("envc")), textured_env=False))
+
+
+@pytest.fixture(scope="session")
 def gpu(built):
     import torch
     assert torch.cuda.is_available(), "GPU tests need a visible MI355X"

@@ -27,3 +27,22 @@ def test_sincos_port_matches_glibc(checker, stride, limit):
     out = subprocess.run([checker, str(stride), limit], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout + out.stderr
     assert " 0 mismatches" in out.stdout
+
+
+@pytest.fixture(scope="module")
+def inv_checker(tmp_path_factory):
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    exe = str(tmp_path_factory.mktemp("libm_inv") / "libm_inv_check")
+    subprocess.check_call([hipcc, "-O2", "-std=c++17", "-ffp-contract=off", "-fno-builtin", "-o", exe,
+                           os.path.join(HERE, "native", "libm_inv_check.cpp")])
+    return exe
+
+
+# Exhaustive runs (stride 1) in this container: acosf 2.13e9 values over [-1, 1] (+ beyond),
+# atanf all 4.28e9 non-NaN-payload patterns, atan2f 3e8 random pairs: 0 mismatches.
+@pytest.mark.parametrize("args", [("acos", "101"), ("atan", "1009"), ("atan2", "3000000", "5")])
+def test_inverse_trig_ports_match_glibc(inv_checker, args):
+    """glibc 2.35 acosf / atanf / atan2f restated in dmath.h (environment light mapping)."""
+    out = subprocess.run([inv_checker, *args], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert " 0 mismatches" in out.stdout
