@@ -278,6 +278,52 @@ NHD float glibc_atan2f(float y, float x) {
     return (z - pi_lo) - pi;
 }
 
+// glibc 2.35 logf (sysdeps/ieee754/flt-32/e_logf.c, table e_logf_data.c, 16 intervals), in
+// the form x86-64 glibc runs on FMA/AVX2 hosts (the __logf_fma ifunc: the double-precision
+// steps contracted to fused multiply-adds).  SampleExponentialDecay (sampling.cpp:60-62).
+NHD float glibc_logf(float x) {
+    struct LogfT { double invc, logc; };
+    const LogfT T[16] = {
+        {0x1.661ec79f8f3bep+0, -0x1.57bf7808caadep-2}, {0x1.571ed4aaf883dp+0, -0x1.2bef0a7c06ddbp-2},
+        {0x1.49539f0f010bp+0, -0x1.01eae7f513a67p-2},  {0x1.3c995b0b80385p+0, -0x1.b31d8a68224e9p-3},
+        {0x1.30d190c8864a5p+0, -0x1.6574f0ac07758p-3}, {0x1.25e227b0b8eap+0, -0x1.1aa2bc79c81p-3},
+        {0x1.1bb4a4a1a343fp+0, -0x1.a4e76ce8c0e5ep-4}, {0x1.12358f08ae5bap+0, -0x1.1973c5a611cccp-4},
+        {0x1.0953f419900a7p+0, -0x1.252f438e10c1ep-5}, {0x1p+0, 0x0p+0},
+        {0x1.e608cfd9a47acp-1, 0x1.aa5aa5df25984p-5},  {0x1.ca4b31f026aap-1, 0x1.c5e53aa362eb4p-4},
+        {0x1.b2036576afce6p-1, 0x1.526e57720db08p-3},  {0x1.9c2d163a1aa2dp-1, 0x1.bc2860d22477p-3},
+        {0x1.886e6037841edp-1, 0x1.1058bc8a07ee1p-2},  {0x1.767dcf5534862p-1, 0x1.4043057b6ee09p-2}};
+    const double Ln2 = 0x1.62e42fefa39efp-1, A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2,
+                 A2 = -0x1.ffffef20a4123p-2;
+    uint32_t ix = ubits(x);
+    if (ix == 0x3f800000u) return 0.f;
+    if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) {
+        if (ix * 2 == 0) return -__builtin_inff();
+        if (ix == 0x7f800000u) return x;
+        if ((ix & 0x80000000u) || ix * 2 >= 0xff000000u) return __builtin_nanf("");
+        ix = ubits(x * 0x1p23f);  // subnormal
+        ix -= 23u << 23;
+    }
+    const uint32_t tmp = ix - 0x3f330000u;
+    const int i = (int)((tmp >> 19) % 16);
+    const int k = (int32_t)tmp >> 23;
+    const uint32_t iz = ix - (tmp & 0xff800000u);
+    double invc = i == 0 ? T[0].invc : 0.0, logc = i == 0 ? T[0].logc : 0.0;
+#pragma unroll
+    for (int j = 1; j < 16; ++j)
+        if (i == j) {
+            invc = T[j].invc;
+            logc = T[j].logc;
+        }
+    const double z = (double)fbits(iz);
+    const double r = __builtin_fma(z, invc, -1.0);
+    const double y0 = __builtin_fma((double)k, Ln2, logc);
+    const double r2 = r * r;
+    double y = __builtin_fma(r, A1, A2);
+    y = __builtin_fma(r2, A0, y);
+    y = __builtin_fma(r2, y, r + y0);
+    return (float)y;
+}
+
 ND float rng_float(uint32_t& y) {
     y = xorshift(y);
     float f = (float)(uint32_t)(y * 0x9E3779BBu) * 2.3283064365386963e-10f;

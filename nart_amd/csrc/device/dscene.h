@@ -77,6 +77,19 @@ struct DMesh {
     uint32_t priority;
 };
 
+// Camera medium (media.h:98-120).  maj[] mirrors the reference's Medium layout after
+// MajorantGrid::majorants[1]: {majorant * sigma_maj, sigma_maj, boundsMin, boundsMax}, because
+// RayMajorantIterator::Next indexes past the 1-entry majorant array (media.cpp:241, 250-251).
+struct DMedium {
+    int32_t present;
+    uint32_t rx, ry, rz;  // uint8_t resolutions of DensityGrid (truncated as in scene.cpp:866)
+    float bmin[3], bmax[3];
+    float sigma_a, sigma_s;
+    float Le[3];
+    float maj[8];
+    const float* density;
+};
+
 struct DScene {
     const BVHNode* nodes;
     const float4* tri_isect;
@@ -94,6 +107,7 @@ struct DScene {
     int32_t geometry_visible;// 0 when the reference octree's root is a leaf (bvh.cpp:131, Q14)
     float cam_m[16];
     float cam_tan;           // tan(radians(fov)) (host libm, as the reference)
+    DMedium medium;
 };
 
 }  // namespace nd

@@ -1,0 +1,227 @@
+// Volume integrator (volumeintegrator.cpp:3-84): delta tracking through the camera medium's
+// width-1 majorant grid (media.h:128-181, media.cpp:3-324), isotropic scattering
+// (UniformSampleSphere, sampling.cpp:33-45), escape to the lights.  No surfaces are
+// intersected: the reference's integrator never calls Scene::Intersect.
+//
+// One lane per traced pixel walks its spp samples in order on its RNG stream (the same slot
+// layout as k_render); the kernel needs no BVH and no LDS.
+#pragma once
+
+#include "kernels.h"
+
+namespace nd {
+
+ND f3 uniform_sample_sphere(f2 smp) {  // sampling.cpp:33-45 (pdf unused by the caller)
+    const float theta = glibc_acosf(1.f - (2.f * smp.x));
+    const float phi = smp.y * ND_TWO_PI;
+    const float cosTheta = glibc_cosf(theta), sinTheta = glibc_sinf(theta);
+    const float cosPhi = glibc_cosf(phi), sinPhi = glibc_sinf(phi);
+    return F3(sinTheta * cosPhi, sinTheta * sinPhi, cosTheta);
+}
+
+NHD float dg_at(const DMedium& m, uint32_t x, uint32_t y, uint32_t z) {  // media.cpp:3-7
+    return m.density[(m.rx * m.ry * z) + (m.rx * y) + x];
+}
+NHD float dg_lookup(const DMedium& m, f3 p) {  // media.cpp:10-45
+    const float x = gmin(gmax(0.f, p.x), 0.999f) * (float)((int)m.rx - 1);
+    const uint32_t loX = (uint8_t)(uint32_t)x, hiX = (uint8_t)(loX + 1);
+    const float xD = (x - (float)loX);
+    const float y = gmin(gmax(0.f, p.y), 0.999f) * (float)((int)m.ry - 1);
+    const uint32_t loY = (uint8_t)(uint32_t)y, hiY = (uint8_t)(loY + 1);
+    const float yD = (y - (float)loY);
+    const float z = gmin(gmax(0.f, p.z), 0.999f) * (float)((int)m.rz - 1);
+    const uint32_t loZ = (uint8_t)(uint32_t)z, hiZ = (uint8_t)(loZ + 1);
+    const float zD = (z - (float)loZ);
+    const float x0 = gmix(dg_at(m, loX, loY, loZ), dg_at(m, hiX, loY, loZ), xD);
+    const float x1 = gmix(dg_at(m, loX, loY, hiZ), dg_at(m, hiX, loY, hiZ), xD);
+    const float x2 = gmix(dg_at(m, loX, hiY, loZ), dg_at(m, hiX, hiY, loZ), xD);
+    const float x3 = gmix(dg_at(m, loX, hiY, hiZ), dg_at(m, hiX, hiY, hiZ), xD);
+    const float y0 = gmix(x0, x2, yD);
+    const float y1 = gmix(x1, x3, yD);
+    return gmix(y0, y1, zD);
+}
+
+struct MajIter {  // RayMajorantIterator (media.cpp:138-255) for a width-1 grid
+    float tCurrent, tMax;
+    uint32_t idx;
+    f3 next, cross;
+    int step[3];
+};
+
+// Medium::SampleRay (media.cpp:281-324) + the iterator constructor.
+ND bool medium_sample_ray(const DMedium& m, f3 o, f3 d, MajIter& it) {
+    float tMin = -__builtin_inff(), tMax = __builtin_inff();
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const f3 n = F3(i == 0 ? 1.f : 0.f, i == 1 ? 1.f : 0.f, i == 2 ? 1.f : 0.f);
+        float slabMin = (m.bmin[i] - dot(o, n)) / dot(d, n);
+        float slabMax = (m.bmax[i] - dot(o, n)) / dot(d, n);
+        if (slabMin > slabMax) {
+            const float t = slabMin;
+            slabMin = slabMax;
+            slabMax = t;
+        }
+        if (slabMin > tMax || tMin > slabMax) return false;
+        tMin = gmax(tMin, slabMin);
+        tMax = gmin(tMax, slabMax);
+    }
+    const f3 bmin = F3(m.bmin[0], m.bmin[1], m.bmin[2]), bmax = F3(m.bmax[0], m.bmax[1], m.bmax[2]);
+    it.tMax = tMax;
+    it.tCurrent = gmax(0.f, tMin);
+    f3 pE = add(o, muls(d, it.tCurrent));
+    f3 pX = add(o, muls(d, tMax));
+    const f3 bs = sub(bmax, bmin);
+    pE = sub(pE, bmin);
+    pE = F3(pE.x / bs.x, pE.y / bs.y, pE.z / bs.z);
+    pE = F3(gmax(gmin(pE.x, 0.999999f), 0.f), gmax(gmin(pE.y, 0.999999f), 0.f), gmax(gmin(pE.z, 0.999999f), 0.f));
+    pE = muls(pE, 1.f);
+    it.idx = 0;
+    pX = sub(pX, bmin);
+    pX = F3(pX.x / bs.x, pX.y / bs.y, pX.z / bs.z);
+    pX = F3(gmax(gmin(pX.x, 0.999999f), 0.f), gmax(gmin(pX.y, 0.999999f), 0.f), gmax(gmin(pX.z, 0.999999f), 0.f));
+    pX = muls(pX, 1.f);
+    f3 gD = normalize(sub(pX, pE));
+    if (pX.x == pE.x && pX.y == pE.y && pX.z == pE.z) gD = F3(1.f, 0.f, 0.f);
+    f3 cd = F3(gabs(((1.f / gD.x) * 1.f) * bs.x), gabs(((1.f / gD.y) * 1.f) * bs.y), gabs(((1.f / gD.z) * 1.f) * bs.z));
+    if (gD.x == 0.f) cd.x = __builtin_inff();
+    if (gD.y == 0.f) cd.y = __builtin_inff();
+    if (gD.z == 0.f) cd.z = __builtin_inff();
+    it.cross = cd;
+    float t3[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float pe = comp(pE, i), g = comp(gD, i);
+        if (comp(d, i) >= 0.f) t3[i] = gabs((ceilf(pe + 0.00001f) - pe) / g);
+        else t3[i] = gabs((floorf(pe - 0.00001f) - pe) / g);
+        if (g == 0.f) t3[i] = __builtin_inff();
+    }
+    it.next = muls(mul(F3(t3[0], t3[1], t3[2]), bs), 1.f);
+    it.step[0] = gD.x < 0.f ? -1 : 1;
+    it.step[1] = gD.y < 0.f ? -1 : 1;
+    it.step[2] = gD.z < 0.f ? -1 : 1;
+    return true;
+}
+
+ND bool maj_next(const DMedium& m, MajIter& it, float& sigma, float& t0, float& t1) {  // media.cpp:214-255
+    if (it.tCurrent + 0.0001f > it.tMax) return false;
+    uint32_t choice = 0;
+    if (it.next.x < it.next.y) choice += 4;
+    if (it.next.x < it.next.z) choice += 2;
+    if (it.next.y < it.next.z) choice += 1;
+    // choiceMap {2, 1, 0, 1, 2, 0, 0, 0}
+    const int index = (choice == 0 || choice == 4) ? 2 : (choice == 1 || choice == 3) ? 1 : 0;
+    const float dt = index == 0 ? it.next.x : index == 1 ? it.next.y : it.next.z;
+    if (it.idx > 7) return false;  // past the Medium object: undefined in the reference
+    float sm = m.maj[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j)
+        if ((int)it.idx == j) sm = m.maj[j];
+    sigma = sm;
+    t0 = it.tCurrent;
+    t1 = it.tCurrent + dt;
+    it.next = sub(it.next, F3(dt, dt, dt));
+    if (index == 0) it.next.x = it.cross.x;
+    else if (index == 1) it.next.y = it.cross.y;
+    else it.next.z = it.cross.z;
+    const int st = index == 0 ? it.step[0] : index == 1 ? it.step[1] : it.step[2];
+    it.idx += st > 0 ? 1u : 0u;
+    it.tCurrent += dt;
+    return true;
+}
+
+// VolumeIntegrator::Li_alpha with SampleT_maj inlined (T_maj only feeds an unused callback
+// argument, so its exp() factors are not evaluated).
+ND f4 li_volume(const DScene& S, const RenderArgs& A, uint32_t& rng, f3 o, f3 d) {
+    const DMedium& m = S.medium;
+    f3 L = F3(0.f, 0.f, 0.f);
+    const f3 beta = F3(1.f, 1.f, 1.f);
+    uint32_t bounce = 0;
+    for (;;) {
+        bool scattered = false, terminated = false;
+        (void)rng_float(rng);  // u: passed to SampleT_maj, unused there
+        float uMode = rng_float(rng);
+        MajIter it;
+        if (m.present && medium_sample_ray(m, o, d, it)) {
+            const f3 ro = o, rd = d;  // SampleT_maj's copy of the ray
+            bool done = false;
+            while (!done) {
+                float sigma, t0, t1;
+                if (!maj_next(m, it, sigma, t0, t1)) break;
+                float tMin = t0;
+                for (;;) {
+                    const float t = tMin + (-glibc_logf(1.f - rng_float(rng)) / sigma);
+                    if (!(t < t1)) break;
+                    const f3 p = add(ro, muls(rd, t));
+                    if (p.x < m.bmin[0] || p.y < m.bmin[1] || p.z < m.bmin[2] || p.x > m.bmax[0] || p.y > m.bmax[1] ||
+                        p.z > m.bmax[2]) {
+                        done = true;
+                        break;
+                    }
+                    const f3 bmin = F3(m.bmin[0], m.bmin[1], m.bmin[2]);
+                    const f3 bs = sub(F3(m.bmax[0], m.bmax[1], m.bmax[2]), bmin);
+                    const f3 q0 = sub(p, bmin);
+                    const float density = dg_lookup(m, F3(q0.x / bs.x, q0.y / bs.y, q0.z / bs.z));
+                    const float sa = m.sigma_a * density, ss = m.sigma_s * density;
+                    const float pAbsorb = sa / sigma;
+                    const float pScatter = ss / sigma;
+                    if (uMode < pAbsorb) {
+                        terminated = true;
+                        L = add(L, mul(muls(F3(m.Le[0], m.Le[1], m.Le[2]), density), beta));
+                        done = true;
+                        break;
+                    } else if (uMode < pAbsorb + pScatter) {
+                        if (bounce++ > A.bounces) {
+                            terminated = true;
+                            done = true;
+                            break;
+                        }
+                        const float a = rng_float(rng);
+                        const float b = rng_float(rng);
+                        o = p;
+                        d = uniform_sample_sphere(F2(a, b));
+                        scattered = true;
+                        done = true;
+                        break;
+                    }
+                    uMode = rng_float(rng);  // null collision
+                    tMin = t;
+                }
+            }
+        }
+        if (terminated) break;
+        if (scattered) continue;
+        float lightTMax = __builtin_inff();
+        f3 Le = F3(0.f, 0.f, 0.f);
+        for (uint32_t j = 0; j < S.num_lights; ++j) {
+            float lt = __builtin_inff();
+            const f3 Li = light_li(S, S.lights[j], o, d, nullptr, lt);
+            if (lt < lightTMax) {
+                Le = Li;
+                lightTMax = lt;
+            }
+        }
+        L = add(L, mul(Le, beta));
+        break;
+    }
+    return F4(L.x, L.y, L.z, 1.f);
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(256) void k_render_volume(DScene S, RenderArgs A) {
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot >= A.n_slots) return;
+    const uint32_t xy = A.slot_xy[slot];
+    const uint32_t px = xy & 0xFFFFu, py = xy >> 16;
+    uint32_t rng = A.rng0[slot];
+    const float2* smp = A.samples + (size_t)slot * A.spp;
+    float4* out = A.Lout + (size_t)slot * A.spp;
+    for (uint32_t s = 0; s < A.spp; ++s) {
+        const float2 sm = smp[s];
+        const Ray r = cast_ray(S, F2(sm.x, sm.y), A.W, A.H, px, py);
+        const f4 L = li_volume(S, A, rng, r.o, r.d);
+        out[s] = make_float4(L.x, L.y, L.z, L.w);
+    }
+    if (COUNT) atomicAdd(&A.counters[0], (unsigned long long)A.spp);
+}
+
+}  // namespace nd

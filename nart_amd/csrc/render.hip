@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../../include/nart_hip.h"
+#include "device/volume.h"
 #include "device/wavefront.h"
 #include "host/bvh_build.h"
 
@@ -34,6 +35,7 @@ struct nart_ctx {
     void* d_texs = nullptr;
     void* d_tex_pool = nullptr;
     void* d_envs = nullptr;
+    void* d_density = nullptr;
     std::vector<void*> env_bufs;  // Piecewise2DDistribution tables
     // work buffers
     size_t cap_slot_bytes = 0, cap_misc = 0;
@@ -181,14 +183,57 @@ int build_env(nart_ctx* ctx, const nart_texture& t, DEnvDist& d) {
     return NART_OK;
 }
 
+// Camera medium: density grid upload + the width-1 MajorantGrid (media.cpp:47-130) on the host.
+int build_medium(nart_ctx* ctx, const nart_medium& bm, DMedium& m) {
+    std::memset(&m, 0, sizeof(m));
+    if (!bm.present) return NART_OK;
+    m.present = 1;
+    m.rx = (uint8_t)bm.res[0];  // DensityGrid(uint8_t, uint8_t, uint8_t, ...) (scene.cpp:866-868)
+    m.ry = (uint8_t)bm.res[1];
+    m.rz = (uint8_t)bm.res[2];
+    if (m.rx < 2 || m.ry < 2 || m.rz < 2)
+        return fail(ctx, NART_E_UNSUPPORTED, "density grids need >= 2 points per axis (DensityGrid::LookUp reads past the grid)");
+    for (int i = 0; i < 3; ++i) {
+        m.bmin[i] = bm.bounds_min[i];
+        m.bmax[i] = bm.bounds_max[i];
+        m.Le[i] = bm.Le[i];
+    }
+    m.sigma_a = bm.sigma_a;
+    m.sigma_s = bm.sigma_s;
+    const uint32_t npts = bm.res[0] * bm.res[1] * bm.res[2];
+    m.density = bm.density;  // host view for the majorant search below
+    const float sigma_maj = bm.sigma_a + bm.sigma_s;
+    const float mx = ((float)m.rx - 1.f) / 1.f, my = ((float)m.ry - 1.f) / 1.f, mz = ((float)m.rz - 1.f) / 1.f;
+    auto u8min = [](uint32_t a, uint32_t b) { return b < a ? b : a; };
+    const uint32_t x1 = u8min((uint8_t)(uint32_t)std::ceil(mx), m.rx);
+    const uint32_t y1 = u8min((uint8_t)(uint32_t)std::ceil(my), m.ry);
+    const uint32_t z1 = u8min((uint8_t)(uint32_t)std::ceil(mz), m.rz);
+    float majorant = 0.f;
+    for (uint32_t k = 0; k < z1; ++k)
+        for (uint32_t j = 0; j < y1; ++j)
+            for (uint32_t i = 0; i < x1; ++i) majorant = gmax(majorant, dg_at(m, i, j, k));
+    for (int c = 0; c < 8; ++c)
+        majorant = gmax(majorant, dg_lookup(m, F3((c & 4) ? 1.f : 0.f, (c & 2) ? 1.f : 0.f, (c & 1) ? 1.f : 0.f)));
+    m.maj[0] = majorant * sigma_maj;
+    m.maj[1] = sigma_maj;
+    for (int i = 0; i < 3; ++i) {
+        m.maj[2 + i] = bm.bounds_min[i];
+        m.maj[5 + i] = bm.bounds_max[i];
+    }
+    int rc = upload(ctx, ctx->d_density, bm.density, npts);
+    m.density = (const float*)ctx->d_density;
+    return rc;
+}
+
 int check_params(nart_ctx* ctx, const nart_render_params* p) {
     if (!p) return fail(ctx, NART_E_INVALID, "null params");
-    if (p->integrator != NART_INTEGRATOR_PATH)
-        return fail(ctx, NART_E_UNSUPPORTED, "volume integrator not implemented on the device yet");
+    if (p->integrator != NART_INTEGRATOR_PATH && p->integrator != NART_INTEGRATOR_VOLUME)
+        return fail(ctx, NART_E_INVALID, "unknown integrator");
     if (!p->image_width || !p->image_height || !p->bucket_size || !p->spp)
         return fail(ctx, NART_E_INVALID, "imageWidth, imageHeight, bucketSize and spp must be > 0");
     if (!(p->filter_width > 0.f)) return fail(ctx, NART_E_INVALID, "filterWidth must be > 0");
-    if (p->bounces > 32) return fail(ctx, NART_E_UNSUPPORTED, "bounces > 32 not supported");
+    if (p->integrator == NART_INTEGRATOR_PATH && p->bounces > 32)
+        return fail(ctx, NART_E_UNSUPPORTED, "bounces > 32 not supported by the path integrator");
     if (ctx->scene.num_lights == 0)
         return fail(ctx, NART_E_INVALID, "scene has no lights (reference throws in Scene::GetLight)");
     nart_session_geometry g;
@@ -360,7 +405,16 @@ int dispatch_wavefront(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     return c ? run_wavefront<32, true>(ctx, a, st) : run_wavefront<32, false>(ctx, a, st);
 }
 
-int dispatch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
+int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
+    dim3 grid((a.n_slots + 255) / 256), block(256);
+    if (ctx->counters) hipLaunchKernelGGL((k_render_volume<true>), grid, block, 0, st, ctx->scene, a);
+    else hipLaunchKernelGGL((k_render_volume<false>), grid, block, 0, st, ctx->scene, a);
+    HIPCHK(hipGetLastError());
+    return NART_OK;
+}
+
+int dispatch_render(nart_ctx* ctx, const RenderArgs& a, int integrator, hipStream_t st) {
+    if (integrator == NART_INTEGRATOR_VOLUME) return dispatch_volume(ctx, a, st);
     return ctx->variant == 1 ? dispatch_wavefront(ctx, a, st) : dispatch_megakernel(ctx, a, st);
 }
 
@@ -450,7 +504,7 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         rc = launch_latin(ctx, ra, st);
         if (rc) return rc;
         HIPCHK(hipEventRecord(ctx->ev[0], st));
-        rc = dispatch_render(ctx, ra, st);
+        rc = dispatch_render(ctx, ra, p->integrator, st);
         if (rc) return rc;
         HIPCHK(hipEventRecord(ctx->ev[1], st));
         SplatArgs sa;
@@ -536,10 +590,6 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     if (hipFuncSetAttribute((const void*)k_latin_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
         hipSuccess)
         return bail(NART_E_HIP);
-    if (blob->medium.present) {
-        ctx->err = "volume integrator / camera medium not implemented on the device yet";
-        return bail(NART_E_UNSUPPORTED);
-    }
     // reference octree visibility (Q14) + device BVH
     std::vector<uint8_t> mask;
     bool root_leaf = false;
@@ -623,6 +673,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     S.texs = (const DTexture*)ctx->d_texs;
     S.tex_pool = (const uint16_t*)ctx->d_tex_pool;
     S.envs = (const DEnvDist*)ctx->d_envs;
+    if ((rc = build_medium(ctx, blob->medium, S.medium))) return bail(rc);
     S.num_lights = blob->num_lights;
     S.num_tris = blob->num_triangles;
     S.root = bvh.root_code;
@@ -639,7 +690,7 @@ void nart_hip_destroy(nart_ctx* ctx) {
     hipSetDevice(ctx->device);
     void* bufs[] = {ctx->d_nodes, ctx->d_tri_isect, ctx->d_tris, ctx->d_tri_mesh, ctx->d_meshes, ctx->d_mats,
                     ctx->d_lights, ctx->d_texs, ctx->d_tex_pool, ctx->d_slot_xy, ctx->d_rng, ctx->d_samples,
-                    ctx->d_L, ctx->d_bucket_ids, ctx->d_bucket_base, ctx->d_table, ctx->d_counters, ctx->d_wf, ctx->d_envs};
+                    ctx->d_L, ctx->d_bucket_ids, ctx->d_bucket_base, ctx->d_table, ctx->d_counters, ctx->d_wf, ctx->d_envs, ctx->d_density};
     for (void* b : bufs)
         if (b) hipFree(b);
     for (void* b : ctx->env_bufs) hipFree(b);
@@ -763,7 +814,7 @@ int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t
     ra.counters = ctx->d_counters;
     rc = launch_latin(ctx, ra, 0);
     if (rc) return rc;
-    rc = dispatch_render(ctx, ra, 0);
+    rc = dispatch_render(ctx, ra, p->integrator, 0);
     if (rc) return rc;
     HIPCHK(hipMemcpy(out, ctx->d_L, (size_t)n * p->spp * sizeof(float4), hipMemcpyDeviceToHost));
     return NART_OK;

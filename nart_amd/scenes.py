@@ -298,3 +298,48 @@ def environment(directory=None, width=320, height=180, spp=16, textured_env=True
     with open(path, "w") as f:
         json.dump(scene, f, indent=1)
     return path
+
+
+def write_vol(path, bounds_min, bounds_max, density):
+    """.vol medium (scene.cpp:826-864): boundsMin, boundsMax, resolution, density (x fastest)."""
+    d = np.asarray(density, np.float32)
+    rz, ry, rx = d.shape
+    toks = [_fmt(v) for v in list(bounds_min) + list(bounds_max)] + [str(rx), str(ry), str(rz)]
+    toks += [_fmt(v) for v in d.reshape(-1)]
+    with open(path, "w") as f:
+        f.write(" ".join(toks) + "\n")
+
+
+def volume(directory=None, width=320, height=180, spp=16, kind="c5"):
+    """Volume-integrator scenes (volumeintegrator.cpp, media.cpp): the camera sits in a medium
+    box lit by the synthetic sky.  kind "c5": BASELINE C5 (constant density 1, 2x2x2 grid, unit
+    cube, sigma_a 0, sigma_s 8, Le 0, 32 bounces).  kind "emissive": a 4x3x5 density gradient
+    with absorption and emission (every branch of the collision callback)."""
+    d = directory or tempfile.mkdtemp(prefix="nart_vol_")
+    os.makedirs(d, exist_ok=True)
+    sky = os.path.join(d, "sky.exr")
+    write_texture(sky, sky_texture())
+    vol = os.path.join(d, "medium.vol")
+    if kind == "c5":
+        write_vol(vol, (-0.5, -0.5, -0.5), (0.5, 0.5, 0.5), np.ones((2, 2, 2), np.float32))
+        medium = {"filePath": vol, "Le": [0, 0, 0], "sigma_a": 0.0, "sigma_s": 8.0}
+        cam = [1, 0, 0, 0, 0, 0, -1, -2.5, 0, 1, 0, 0, 0, 0, 0, 1]
+        bounces = 32
+    else:
+        z, y, x = np.mgrid[0:5, 0:3, 0:4].astype(np.float32)
+        dens = 0.2 + 0.8 * (x / 3.0) * (1.0 - 0.5 * y / 2.0) + 0.3 * (z / 4.0)
+        write_vol(vol, (-1.0, -0.8, -0.6), (1.2, 0.9, 1.0), dens)
+        medium = {"filePath": vol, "Le": [2.0, 1.2, 0.4], "sigma_a": 1.5, "sigma_s": 3.0}
+        cam = [1, 0, 0, 0.1, 0, 0, -1, -0.5, 0, 1, 0, 0.2, 0, 0, 0, 1]
+        bounces = 6
+    scene = {
+        "renderSessions": [{"imageWidth": width, "imageHeight": height, "bucketSize": 16, "spp": spp,
+                            "bounces": bounces, "filterWidth": 2, "integrator": "volume"}],
+        "camera": {"fov": 30.0, "transform": cam, "medium": medium},
+        "meshes": [],
+        "lights": [{"type": "environment", "Le": {"type": "texture", "filePath": sky}, "intensity": 1.0}],
+    }
+    path = os.path.join(d, "volume_%s.json" % kind)
+    with open(path, "w") as f:
+        json.dump(scene, f, indent=1)
+    return path

@@ -277,6 +277,11 @@ struct oracle_scene {
     size_t* tex_off;
     /* environment distributions per light (Piecewise2DDistribution) */
     struct pw2d { int present; uint32_t w, h; float invW, invH; float *mpdf, *cpdf, *mcdf, *ccdf; } * env;
+    /* camera medium (media.h:98-120): the majorant table is laid out as the reference's Medium
+       members after MajorantGrid::majorants[1] -- {majorant * sigma_maj, sigma_maj, boundsMin,
+       boundsMax} -- because RayMajorantIterator::Next can index past the 1-entry array. */
+    int has_medium;
+    float maj[8];
 };
 
 static int new_node(oracle_scene* s, v3 mn, v3 mx) {
@@ -1235,6 +1240,222 @@ static v4 li_alpha(const oracle_scene* s, worker_t* w, rng_t* rng, ray_t ray, co
     return V4(L.x, L.y, L.z, alpha);
 }
 
+/* ---------------------------------------------------------------- volume integrator */
+static v3 uniform_sample_sphere(v2 smp) { /* sampling.cpp:33-45 (pdf = 1/(4 pi) is unused) */
+    float theta = acosf(1.f - (2.f * smp.x));
+    float phi = smp.y * TWO_PI_F;
+    float cosTheta = cosf(theta);
+    float sinTheta = sinf(theta);
+    float cosPhi = cosf(phi);
+    float sinPhi = sinf(phi);
+    return V3(sinTheta * cosPhi, sinTheta * sinPhi, cosTheta);
+}
+
+static float dg_at(const nart_medium* m, uint8_t x, uint8_t y, uint8_t z) { /* media.cpp:3-7 */
+    uint8_t rx = (uint8_t)m->res[0], ry = (uint8_t)m->res[1];
+    uint32_t index = (uint32_t)((rx * ry * z) + (rx * y) + x);
+    return m->density[index];
+}
+static float dg_lookup(const nart_medium* m, v3 p) { /* media.cpp:10-45, trilinear */
+    uint8_t rx = (uint8_t)m->res[0], ry = (uint8_t)m->res[1], rz = (uint8_t)m->res[2];
+    float x = gmin(gmax(0.f, p.x), 0.999f) * (float)(rx - 1);
+    uint8_t loX = (uint8_t)x, hiX = (uint8_t)(loX + 1);
+    float xD = (x - (float)loX);
+    float y = gmin(gmax(0.f, p.y), 0.999f) * (float)(ry - 1);
+    uint8_t loY = (uint8_t)y, hiY = (uint8_t)(loY + 1);
+    float yD = (y - (float)loY);
+    float z = gmin(gmax(0.f, p.z), 0.999f) * (float)(rz - 1);
+    uint8_t loZ = (uint8_t)z, hiZ = (uint8_t)(loZ + 1);
+    float zD = (z - (float)loZ);
+    float x0 = gmix(dg_at(m, loX, loY, loZ), dg_at(m, hiX, loY, loZ), xD);
+    float x1 = gmix(dg_at(m, loX, loY, hiZ), dg_at(m, hiX, loY, hiZ), xD);
+    float x2 = gmix(dg_at(m, loX, hiY, loZ), dg_at(m, hiX, hiY, loZ), xD);
+    float x3 = gmix(dg_at(m, loX, hiY, hiZ), dg_at(m, hiX, hiY, hiZ), xD);
+    float y0 = gmix(x0, x2, yD);
+    float y1 = gmix(x1, x3, yD);
+    return gmix(y0, y1, zD);
+}
+static uint8_t u8min(uint8_t a, uint8_t b) { return b < a ? b : a; }
+static void build_medium(oracle_scene* s) { /* MajorantGrid ctor, width 1 (media.cpp:47-130) */
+    const nart_medium* m = &s->blob->medium;
+    s->has_medium = m->present;
+    if (!m->present) return;
+    uint8_t rx = (uint8_t)m->res[0], ry = (uint8_t)m->res[1], rz = (uint8_t)m->res[2];
+    float sigma_maj = m->sigma_a + m->sigma_s;
+    float mx = ((float)rx - 1.f) / 1.f, my = ((float)ry - 1.f) / 1.f, mz = ((float)rz - 1.f) / 1.f;
+    uint8_t x1 = u8min((uint8_t)f2u32(ceilf(mx)), rx);
+    uint8_t y1 = u8min((uint8_t)f2u32(ceilf(my)), ry);
+    uint8_t z1 = u8min((uint8_t)f2u32(ceilf(mz)), rz);
+    float majorant = 0.f;
+    for (uint8_t k = 0; k < z1; ++k)
+        for (uint8_t j = 0; j < y1; ++j)
+            for (uint8_t i = 0; i < x1; ++i) majorant = gmax(majorant, dg_at(m, i, j, k));
+    for (int c = 0; c < 8; ++c) {
+        float px = (c & 4) ? 1.f : 0.f, py = (c & 2) ? 1.f : 0.f, pz = (c & 1) ? 1.f : 0.f;
+        majorant = gmax(majorant, dg_lookup(m, V3(px, py, pz)));
+    }
+    s->maj[0] = majorant * sigma_maj;
+    s->maj[1] = sigma_maj;
+    s->maj[2] = m->bounds_min[0]; s->maj[3] = m->bounds_min[1]; s->maj[4] = m->bounds_min[2];
+    s->maj[5] = m->bounds_max[0]; s->maj[6] = m->bounds_max[1]; s->maj[7] = m->bounds_max[2];
+}
+
+typedef struct { /* RayMajorantIterator (media.cpp:138-255), width-1 majorant grid */
+    float tCurrent, tMax;
+    uint32_t currentIndex;
+    v3 nextCrossing, crossDistance;
+    int stepAxis[3];
+} maj_iter_t;
+
+static int medium_sample_ray(const oracle_scene* s, v3 o, v3 d, maj_iter_t* it) { /* media.cpp:281-324 */
+    const nart_medium* m = &s->blob->medium;
+    float tMin = -INF_F, tMax = INF_F;
+    for (int i = 0; i < 3; ++i) {
+        v3 n = V3(i == 0 ? 1.f : 0.f, i == 1 ? 1.f : 0.f, i == 2 ? 1.f : 0.f);
+        float slabMin = (m->bounds_min[i] - dot3(o, n)) / dot3(d, n);
+        float slabMax = (m->bounds_max[i] - dot3(o, n)) / dot3(d, n);
+        if (slabMin > slabMax) { float t = slabMin; slabMin = slabMax; slabMax = t; }
+        if (slabMin > tMax || tMin > slabMax) return 0;
+        tMin = gmax(tMin, slabMin);
+        tMax = gmin(tMax, slabMax);
+    }
+    v3 bmin = V3(m->bounds_min[0], m->bounds_min[1], m->bounds_min[2]);
+    v3 bmax = V3(m->bounds_max[0], m->bounds_max[1], m->bounds_max[2]);
+    it->tMax = tMax;
+    it->tCurrent = gmax(0.f, tMin);
+    v3 pE = add3(o, muls3(d, it->tCurrent));
+    v3 pX = add3(o, muls3(d, tMax));
+    v3 bs = sub3(bmax, bmin);
+    pE = div3(sub3(pE, bmin), bs);
+    pE = V3(gmax(gmin(pE.x, 0.999999f), 0.f), gmax(gmin(pE.y, 0.999999f), 0.f), gmax(gmin(pE.z, 0.999999f), 0.f));
+    pE = muls3(pE, 1.f);
+    it->currentIndex = 0; /* ivec3(pEntering) is 0 in a width-1 grid */
+    pX = div3(sub3(pX, bmin), bs);
+    pX = V3(gmax(gmin(pX.x, 0.999999f), 0.f), gmax(gmin(pX.y, 0.999999f), 0.f), gmax(gmin(pX.z, 0.999999f), 0.f));
+    pX = muls3(pX, 1.f);
+    v3 gD = normalize3(sub3(pX, pE));
+    if (pX.x == pE.x && pX.y == pE.y && pX.z == pE.z) gD = V3(1.f, 0.f, 0.f);
+    v3 cd = V3(gabs(((1.f / gD.x) * 1.f) * bs.x), gabs(((1.f / gD.y) * 1.f) * bs.y), gabs(((1.f / gD.z) * 1.f) * bs.z));
+    if (gD.x == 0.f) cd.x = INF_F;
+    if (gD.y == 0.f) cd.y = INF_F;
+    if (gD.z == 0.f) cd.z = INF_F;
+    it->crossDistance = cd;
+    float t3[3];
+    for (int i = 0; i < 3; ++i) {
+        float pe = v3get(pE, i), g = v3get(gD, i);
+        if (v3get(d, i) >= 0.f) t3[i] = gabs((ceilf(pe + 0.00001f) - pe) / g);
+        else t3[i] = gabs((floorf(pe - 0.00001f) - pe) / g);
+        if (g == 0.f) t3[i] = INF_F;
+    }
+    it->nextCrossing = muls3(mul3(V3(t3[0], t3[1], t3[2]), bs), 1.f);
+    it->stepAxis[0] = gD.x < 0.f ? -1 : 1;
+    it->stepAxis[1] = gD.y < 0.f ? -1 : 1;
+    it->stepAxis[2] = gD.z < 0.f ? -1 : 1;
+    return 1;
+}
+static int maj_next(const oracle_scene* s, maj_iter_t* it, float* sigma, float* t0, float* t1) {
+    if (it->tCurrent + 0.0001f > it->tMax) return 0;
+    static const uint8_t choiceMap[8] = {2, 1, 0, 1, 2, 0, 0, 0};
+    uint8_t choice = 0;
+    if (it->nextCrossing.x < it->nextCrossing.y) choice += 4;
+    if (it->nextCrossing.x < it->nextCrossing.z) choice += 2;
+    if (it->nextCrossing.y < it->nextCrossing.z) choice += 1;
+    int index = choiceMap[choice];
+    float dt = v3get(it->nextCrossing, index);
+    if (it->currentIndex > 7) return 0; /* beyond the Medium object: undefined in the reference */
+    *sigma = s->maj[it->currentIndex];
+    *t0 = it->tCurrent;
+    *t1 = it->tCurrent + dt;
+    it->nextCrossing = sub3(it->nextCrossing, V3(dt, dt, dt));
+    if (index == 0) it->nextCrossing.x = it->crossDistance.x;
+    else if (index == 1) it->nextCrossing.y = it->crossDistance.y;
+    else it->nextCrossing.z = it->crossDistance.z;
+    it->currentIndex += (uint32_t)(it->stepAxis[index] > 0 ? 1 : 0);
+    it->tCurrent += dt;
+    return 1;
+}
+
+/* VolumeIntegrator::Li_alpha (volumeintegrator.cpp:3-84) with SampleT_maj (media.h:128-181) */
+static v4 li_volume(const oracle_scene* s, rng_t* rng, ray_t ray, const nart_render_params* p) {
+    const nart_medium* m = &s->blob->medium;
+    v3 L = V3(0.f, 0.f, 0.f), beta = V3(1.f, 1.f, 1.f);
+    uint32_t bounce = 0;
+    for (;;) {
+        int scattered = 0, terminated = 0;
+        (void)rng_float(rng); /* u: passed to SampleT_maj, unused there */
+        float uMode = rng_float(rng);
+        maj_iter_t it;
+        if (s->has_medium && medium_sample_ray(s, ray.o, ray.d, &it)) {
+            const v3 o = ray.o, d = ray.d; /* SampleT_maj's copy of the ray */
+            int done = 0;
+            while (!done) {
+                float sigma, t0, t1;
+                if (!maj_next(s, &it, &sigma, &t0, &t1)) break;
+                float tMin = t0;
+                for (;;) {
+                    float t = tMin + (-logf(1.f - rng_float(rng)) / sigma);
+                    if (t < t1) {
+                        v3 pp = add3(o, muls3(d, t));
+                        if (pp.x < m->bounds_min[0] || pp.y < m->bounds_min[1] || pp.z < m->bounds_min[2] ||
+                            pp.x > m->bounds_max[0] || pp.y > m->bounds_max[1] || pp.z > m->bounds_max[2]) {
+                            done = 1;
+                            break;
+                        }
+                        v3 q = div3(sub3(pp, V3(m->bounds_min[0], m->bounds_min[1], m->bounds_min[2])),
+                                    sub3(V3(m->bounds_max[0], m->bounds_max[1], m->bounds_max[2]),
+                                         V3(m->bounds_min[0], m->bounds_min[1], m->bounds_min[2])));
+                        float density = dg_lookup(m, q);
+                        float sa = m->sigma_a * density, ss = m->sigma_s * density;
+                        v3 mLe = muls3(V3(m->Le[0], m->Le[1], m->Le[2]), density);
+                        float pAbsorb = sa / sigma;
+                        float pScatter = ss / sigma;
+                        if (uMode < pAbsorb) {
+                            terminated = 1;
+                            L = add3(L, mul3(mLe, beta));
+                            done = 1;
+                            break;
+                        } else if (uMode < pAbsorb + pScatter) {
+                            if (bounce++ > p->bounces) {
+                                terminated = 1;
+                                done = 1;
+                                break;
+                            }
+                            float a = rng_float(rng);
+                            float b = rng_float(rng);
+                            ray.o = pp;
+                            ray.d = uniform_sample_sphere(V2(a, b));
+                            scattered = 1;
+                            done = 1;
+                            break;
+                        } else {
+                            uMode = rng_float(rng);
+                        }
+                        tMin = t; /* null collision: continue from here (T_maj only feeds the unused callback argument) */
+                    } else {
+                        break;
+                    }
+                }
+            }
+        }
+        if (terminated) break;
+        if (scattered) continue;
+        float lightTMax = INF_F;
+        v3 Le = V3(0.f, 0.f, 0.f);
+        for (uint8_t j = 0; j < s->blob->num_lights; ++j) {
+            lisect_t li;
+            li.tMax = INF_F;
+            v3 Li = light_li(s, j, &li, ray.o, ray.d, NULL);
+            if (li.tMax < lightTMax) {
+                Le = Li;
+                lightTMax = li.tMax;
+            }
+        }
+        L = add3(L, mul3(Le, beta));
+        break;
+    }
+    return V4(L.x, L.y, L.z, 1.f);
+}
+
 /* ---------------------------------------------------------------- camera */
 static ray_t cast_ray(const oracle_scene* s, v2 smp, uint32_t W, uint32_t H, uint32_t x, uint32_t y) { /* pinholecamera.cpp:9-40 */
     const nart_camera* c = &s->blob->camera;
@@ -1310,7 +1531,7 @@ static void render_tile(const oracle_scene* s, worker_t* w, const nart_render_pa
             latin_square(&rng, p->spp, smp);
             for (uint32_t i = 0; i < p->spp; ++i) {
                 ray_t ray = cast_ray(s, smp[i], p->image_width, p->image_height, x, y);
-                v4 L = li_alpha(s, w, &rng, ray, p);
+                v4 L = p->integrator == NART_INTEGRATOR_VOLUME ? li_volume(s, &rng, ray, p) : li_alpha(s, w, &rng, ray, p);
                 v2 sc = V2((float)(x + ss->fb) + smp[i].x, (float)(y + ss->fb) + smp[i].y);
                 add_sample(ss, p, sc, L, tile);
             }
@@ -1348,7 +1569,8 @@ static void* worker_main(void* arg) {
 static int check_params(const oracle_scene* s, const nart_render_params* p) {
     if (!p->image_width || !p->image_height || !p->bucket_size || !p->spp) return NART_E_INVALID;
     if (p->filter_width <= 0.f) return NART_E_INVALID;
-    if (p->integrator != NART_INTEGRATOR_PATH) return NART_E_UNSUPPORTED;
+    if (p->integrator == NART_INTEGRATOR_VOLUME && s->has_medium && (s->blob->medium.res[0] % 256 < 2 || s->blob->medium.res[1] % 256 < 2 || s->blob->medium.res[2] % 256 < 2))
+        return NART_E_UNSUPPORTED; /* DensityGrid::LookUp reads past the grid below 2 points per axis */
     if (p->bounces > 64) return NART_E_UNSUPPORTED;
     if (s->blob->num_lights == 0) return NART_E_INVALID; /* reference throws in GetLight */
     return NART_OK;
@@ -1428,7 +1650,7 @@ int oracle_render_samples(oracle_scene* s, const nart_render_params* p, uint32_t
             size_t base = ((size_t)(y - y0) * w + (x - x0)) * p->spp;
             for (uint32_t i = 0; i < p->spp; ++i) {
                 ray_t ray = cast_ray(s, smp[i], p->image_width, p->image_height, x, y);
-                v4 L = li_alpha(s, &wk, &rng, ray, p);
+                v4 L = p->integrator == NART_INTEGRATOR_VOLUME ? li_volume(s, &rng, ray, p) : li_alpha(s, &wk, &rng, ray, p);
                 float* o = out + (base + i) * 4;
                 o[0] = L.x; o[1] = L.y; o[2] = L.z; o[3] = L.w;
                 if (uv) { uv[(base + i) * 2] = smp[i].x; uv[(base + i) * 2 + 1] = smp[i].y; }
@@ -1538,6 +1760,7 @@ int oracle_create(const nart_scene_blob* blob, oracle_scene** out) {
     }
     build_bvh(s);
     build_env(s);
+    build_medium(s);
     *out = s;
     return NART_OK;
 }

@@ -58,6 +58,14 @@ def env_const_scene(built, tmp_path_factory):
 
 
 @pytest.fixture(scope="session")
+def volume_scenes(built, tmp_path_factory):
+    import nart_amd
+    from nart_amd import scenes
+    return {k: nart_amd.Scene(scenes.volume(str(tmp_path_factory.mktemp("vol_" + k)), kind=k))
+            for k in ("c5", "emissive")}
+
+
+@pytest.fixture(scope="session")
 def gpu(built):
     import torch
     assert torch.cuda.is_available(), "GPU tests need a visible MI355X"

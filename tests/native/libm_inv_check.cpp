@@ -3,6 +3,7 @@
 //   libm_inv_check acos STRIDE        every STRIDE-th float bit pattern in [-1, 1] (and beyond)
 //   libm_inv_check atan STRIDE        every STRIDE-th bit pattern of both signs
 //   libm_inv_check atan2 N SEED       N random (y, x) pairs: unit vectors, wide exponents, specials
+//   libm_inv_check log STRIDE         every STRIDE-th positive float bit pattern
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -17,7 +18,19 @@ int main(int argc, char** argv) {
     if (argc < 3) return 2;
     const char* fn = argv[1];
     unsigned long n = 0, bad = 0;
-    if (!std::strcmp(fn, "acos") || !std::strcmp(fn, "atan")) {
+    if (!std::strcmp(fn, "log")) {  // every STRIDE-th positive pattern up to +inf, and -1, -0
+        unsigned stride = (unsigned)std::strtoul(argv[2], nullptr, 10);
+        for (unsigned b = 0; b <= 0x7f800000u; b += stride) {
+            float x;
+            std::memcpy(&x, &b, 4);
+            float r = nd::glibc_logf(x), h = logf(x);
+            if (!same(r, h)) {
+                if (bad < 5) std::printf("mismatch log(%a) port=%a glibc=%a\n", x, r, h);
+                ++bad;
+            }
+            ++n;
+        }
+    } else if (!std::strcmp(fn, "acos") || !std::strcmp(fn, "atan")) {
         unsigned stride = (unsigned)std::strtoul(argv[2], nullptr, 10);
         bool acos = !std::strcmp(fn, "acos");
         unsigned top = acos ? 0x3f800010u : 0x7f800001u;

@@ -141,6 +141,26 @@ def test_environment_per_sample(gpu, env_scene):
     assert _bits_equal(g, r), _report(g, r)
 
 
+@pytest.mark.parametrize("kind", ["c5", "emissive"])
+def test_volume_integrator(gpu, volume_scenes, kind):
+    """VolumeIntegrator::Li_alpha (volumeintegrator.cpp): delta tracking with the width-1
+    majorant grid, trilinear density, absorption/emission, isotropic scattering (acosf, logf
+    ports), escape to the textured environment light."""
+    sc = volume_scenes[kind]
+    p = _params(sc, 96, 64, 8)
+    g = nart_amd.HipRenderer(sc).render(p)
+    r = oracle.Oracle(sc).render(p)
+    assert _bits_equal(g, r), _report(g, r)
+
+
+def test_volume_per_sample(gpu, volume_scenes):
+    sc = volume_scenes["c5"]
+    p = _params(sc, 320, 180, 32)
+    g = nart_amd.HipRenderer(sc).render_samples(p, 140, 70, 16, 12)
+    r = oracle.Oracle(sc).render_samples(p, 140, 70, 16, 12)
+    assert _bits_equal(g, r), _report(g, r)
+
+
 @pytest.mark.parametrize("bounces", [0, 1, 2, 12, 20])
 def test_bounce_limits(glass_gpu, glass_oracle, glass_scene, bounces):
     """Bounce caps (pathintegrator.cpp:165): none, shallow, and the 16/32-entry list builds."""

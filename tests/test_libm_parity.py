@@ -40,9 +40,11 @@ def inv_checker(tmp_path_factory):
 
 # Exhaustive runs (stride 1) in this container: acosf 2.13e9 values over [-1, 1] (+ beyond),
 # atanf all 4.28e9 non-NaN-payload patterns, atan2f 3e8 random pairs: 0 mismatches.
-@pytest.mark.parametrize("args", [("acos", "101"), ("atan", "1009"), ("atan2", "3000000", "5")])
+# logf (FMA form): all 2.14e9 positive patterns, 0 mismatches.
+@pytest.mark.parametrize("args", [("acos", "101"), ("atan", "1009"), ("atan2", "3000000", "5"), ("log", "211")])
 def test_inverse_trig_ports_match_glibc(inv_checker, args):
-    """glibc 2.35 acosf / atanf / atan2f restated in dmath.h (environment light mapping)."""
+    """glibc 2.35 acosf / atanf / atan2f / logf restated in dmath.h (environment light mapping,
+    UniformSampleSphere, SampleExponentialDecay)."""
     out = subprocess.run([inv_checker, *args], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout + out.stderr
     assert " 0 mismatches" in out.stdout

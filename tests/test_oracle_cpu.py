@@ -184,3 +184,27 @@ def test_splat_wraps_at_bucket_edge(glass_scene):
     o = oracle.Oracle(glass_scene)
     tiles = o.render_buckets(p, np.arange(g.n_buckets_x * g.n_buckets_y, dtype=np.uint32))
     assert np.isfinite(tiles).all()
+
+
+def test_volume_oracle_properties(built, tmp_path):
+    """Volume integrator restatement: alpha is always 1 (volumeintegrator.cpp:11,83); with the
+    medium removed every sample returns the env light seen along the camera ray."""
+    import json
+    import numpy as np
+    import nart_amd
+    import oracle
+    from nart_amd import scenes
+    path = scenes.volume(str(tmp_path / "v"), kind="emissive")
+    sc = nart_amd.Scene(path)
+    p = nart_amd.load_sessions(path)[0]
+    p.image_width, p.image_height, p.spp = 24, 16, 4
+    out = oracle.Oracle(sc).render_samples(p, 0, 0, 24, 16)
+    assert np.all(out[..., 3] == 1.0) and np.isfinite(out).all()
+    j = json.load(open(path))
+    del j["camera"]["medium"]
+    path2 = str(tmp_path / "nomed.json")
+    json.dump(j, open(path2, "w"))
+    sc2 = nart_amd.Scene(path2)
+    out2 = oracle.Oracle(sc2).render_samples(p, 0, 0, 24, 16)
+    assert np.all(out2[..., 3] == 1.0) and (out2[..., :3] > 0).all()
+    assert not np.array_equal(out, out2)
