@@ -123,6 +123,18 @@ def scene_lib():
 
 
 def hip_lib():
+    # NART_HIP_LIB: an alternative build of the same ABI (A/B experiments, tools/ab.sh)
+    alt = os.environ.get("NART_HIP_LIB")
+    if alt:
+        if "libnart_hip.so" not in _libs:
+            scene_lib()  # its directory is on the alternative build's rpath too
+            lib = ctypes.CDLL(os.path.abspath(alt))
+            for fn, (res, args) in _HIP_SIGS.items():
+                f = getattr(lib, fn)
+                f.restype = res
+                f.argtypes = args
+            _libs["libnart_hip.so"] = lib
+        return _libs["libnart_hip.so"]
     return _load("libnart_hip.so", _HIP_SIGS)
 
 

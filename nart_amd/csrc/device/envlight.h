@@ -14,9 +14,11 @@ ND float env_ptn_pdf(const DScene& S, const DLight& L, f2 st) {
     return env_pdf(S.envs[L.env], F2(gmin(st.x, 0.9999f), gmin(st.y, 0.9999f)));
 }
 
-// Light::Li (disklight.cpp:12-23, ringlight.cpp:117-128, environmentlight.cpp:9-28)
+// Light::Li (disklight.cpp:12-23, ringlight.cpp:117-128, environmentlight.cpp:9-28).
+// ENV = false compiles the environment branch out (scenes without one): it costs registers.
+template <bool ENV = true>
 ND f3 light_li(const DScene& S, const DLight& L, f3 p, f3 wi, float* pdf, float& tMax) {
-    if (L.type == NART_LIGHT_ENVIRONMENT) {
+    if (ENV && L.type == NART_LIGHT_ENVIRONMENT) {
         const float theta = glibc_acosf(wi.z);
         float phi = glibc_atan2f(wi.y, wi.x) + ND_PI;
         if (phi > ND_TWO_PI) phi -= ND_TWO_PI;
@@ -39,8 +41,9 @@ ND f3 light_li(const DScene& S, const DLight& L, f3 p, f3 wi, float* pdf, float&
 }
 
 // Light::Sample_Li (disklight.cpp:25-60, ringlight.cpp:130-168)
+template <bool ENV = true>
 ND f3 light_sample_li(const DScene& S, const DLight& L, f3 p, f3& wi, f2 sample, float& pdf, float& tMax) {
-    if (L.type == NART_LIGHT_ENVIRONMENT) {
+    if (ENV && L.type == NART_LIGHT_ENVIRONMENT) {
         // Pattern::Sample (constantpattern.cpp:3-14, texturepattern.cpp:130-158)
         f2 ps = sample;
         f3 Lv;

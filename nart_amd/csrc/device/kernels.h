@@ -84,7 +84,15 @@ struct RenderArgs {
     uint32_t n_slots, spp, bounces, W, H, totalW, stack_depth;
     float gamma;              // roughening factor squared (pathintegrator.cpp:163)
     unsigned long long* counters;  // [5] extend rays, shadow rays, node visits, tri tests, bounces
+    uint32_t lds_nodes;       // BVH nodes [0, lds_nodes) staged in LDS after the stack
 };
+
+// Stage the top BVH nodes (breadth-first prefix) into LDS; every thread of the block calls it.
+ND void stage_nodes(const DScene& S, float4* dst, uint32_t n) {
+    const float4* src = reinterpret_cast<const float4*>(S.nodes);
+    for (uint32_t i = threadIdx.x; i < 4 * n; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+}
 
 // ---------------------------------------------------------------- LatinSquare per pixel
 __global__ __launch_bounds__(256) void k_latin(RenderArgs A) {
@@ -154,13 +162,23 @@ enum { ST_EXT = 0, ST_SH1 = 1, ST_SH2 = 2 };
 // stream.  Each loop iteration traces exactly one ray (extension or shadow) through the
 // shared traversal loop, then advances the lane's path state machine; a lane whose path
 // ends starts its next sample immediately (path regeneration), so lanes of a wave stay busy.
-template <int MAXL, bool COUNT>
-__global__ __launch_bounds__(256) void k_render(DScene S, RenderArgs A) {
+// Min waves per SIMD requested from the register allocator.  Without it the allocator takes
+// >256 registers (VGPR + AGPR) once the environment-light code is inlined and the kernel drops
+// to 1 wave/SIMD (C3 at 64 spp: 260 ms vs 151 ms at 2 waves; 3 waves spills: 178 ms).
+#ifndef NART_RENDER_WAVES
+#define NART_RENDER_WAVES 2
+#endif
+#define NART_RENDER_LB __launch_bounds__(256, NART_RENDER_WAVES)
+template <int MAXL, bool COUNT, bool ENV>
+__global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
     // LDS traversal stack: stack_depth entries of (node code, entry distance) per lane,
     // laid out [depth][lane] so a wave's 64 lanes hit 64 distinct banks.
     extern __shared__ __attribute__((aligned(16))) int s_dyn[];
     int* s_code = s_dyn;
     float* s_tn = reinterpret_cast<float*>(s_dyn + A.stack_depth * blockDim.x);
+    float4* s_nodes = reinterpret_cast<float4*>(s_dyn + 2 * A.stack_depth * blockDim.x);
+    stage_nodes(S, s_nodes, A.lds_nodes);
+    const int nl = (int)A.lds_nodes;
     const int tid = threadIdx.x;
     const uint32_t slot = blockIdx.x * blockDim.x + tid;
     if (slot >= A.n_slots) return;
@@ -219,7 +237,7 @@ __global__ __launch_bounds__(256) void k_render(DScene S, RenderArgs A) {
             Le = F3(0.f, 0.f, 0.f);
             for (uint32_t j = 0; j < S.num_lights; ++j) {
                 float lt = __builtin_inff();
-                f3 Li = light_li(S, S.lights[j], ray.o, ray.d, nullptr, lt);
+                f3 Li = light_li<ENV>(S, S.lights[j], ray.o, ray.d, nullptr, lt);
                 if (lt < lightTMax) {
                     Le = Li;
                     lightTMax = lt;
@@ -235,7 +253,7 @@ __global__ __launch_bounds__(256) void k_render(DScene S, RenderArgs A) {
 
         float bt;
         uint32_t bg;
-        const bool hit = traverse<COUNT>(S, cur, tmax, stage != ST_EXT, bt, bg, sc, stn, stride, cnt);
+        const bool hit = traverse<COUNT>(S, cur, tmax, stage != ST_EXT, bt, bg, sc, stn, stride, cnt, s_nodes, nl);
 
         bool resolve = false;
         if (stage == ST_EXT) {
@@ -270,7 +288,7 @@ __global__ __launch_bounds__(256) void k_render(DScene S, RenderArgs A) {
                     float flip = wi.z > 0.f ? 1.f : -1.f;
                     f3 wW = to_world(bsdf, wi);
                     float lt = __builtin_inff();
-                    f3 Li = light_li(S, Lg, is.p, wW, &lPdf, lt);
+                    f3 Li = light_li<ENV>(S, Lg, is.p, wW, &lPdf, lt);
                     float weight = 1.f;
                     bool add1 = true;
                     if (!(dflags & F_SPECULAR)) {
@@ -292,7 +310,7 @@ __global__ __launch_bounds__(256) void k_render(DScene S, RenderArgs A) {
                 float ly = rng_float(rng);
                 f3 wiW;
                 float lt2 = __builtin_inff();
-                f3 Li2 = light_sample_li(S, Lg, is.p, wiW, F2(lx, ly), lPdf, lt2);
+                f3 Li2 = light_sample_li<ENV>(S, Lg, is.p, wiW, F2(lx, ly), lPdf, lt2);
                 f3 wi2 = to_local(bsdf, wiW);
                 if (lPdf > 0.f) {
                     float sp2 = bsdf_pdf(bsdf, wo, wi2, true, eta_outer);

@@ -175,24 +175,49 @@ __global__ __launch_bounds__(256) void k_wf_trace(DScene S, WFArgs A, uint32_t i
     const size_t N = A.R.n_slots;
     TraceCounters cnt = {0u, 0u};
     uint32_t n_ext = 0, n_sh = 0, n_hit = 0;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gsize) {
-        const uint32_t tag = i < ne ? (A.rq_ext[cur][i] << 2) : A.rq_sh[cur][i - ne];
-        const uint32_t slot = tag >> 2, kind = tag & 3u;
-        const float4 o = A.st.ray_o[kind * N + slot];
-        const float4 d = A.st.ray_d[kind * N + slot];
-        Ray r = make_ray(F3(o.x, o.y, o.z), F3(d.x, d.y, d.z));
-        float bt;
-        uint32_t bg;
-        const bool hit = traverse<COUNT>(S, r, o.w, kind != RK_EXT, bt, bg, sc, stn, blockDim.x, cnt);
-        if (kind == RK_EXT) {
-            A.st.hit[slot] = make_uint2(__float_as_uint(bt), hit ? bg : NO_HIT);
-            if (COUNT) {
-                ++n_ext;
-                n_hit += hit ? 1u : 0u;
+    // Persistent lanes with dynamic ray fetching: a lane whose ray is resolved takes its next
+    // ray (grid-stride order) before the next traversal step, instead of idling until the
+    // slowest ray of its wave is done.
+    uint32_t next = blockIdx.x * blockDim.x + threadIdx.x;
+    bool busy = false;
+    uint32_t slot = 0, kind = 0;
+    Ray r;
+    Trav t;
+    for (;;) {
+        while (!busy && next < n) {
+            const uint32_t tag = next < ne ? (A.rq_ext[cur][next] << 2) : A.rq_sh[cur][next - ne];
+            next += gsize;
+            slot = tag >> 2;
+            kind = tag & 3u;
+            const float4 o = A.st.ray_o[kind * N + slot];
+            const float4 d = A.st.ray_d[kind * N + slot];
+            r = make_ray(F3(o.x, o.y, o.z), F3(d.x, d.y, d.z));
+            if (S.geometry_visible) {
+                trav_begin(S, r, o.w, kind != RK_EXT, t);
+                busy = true;
+            } else {  // nothing to hit
+                if (kind == RK_EXT) A.st.hit[slot] = make_uint2(__float_as_uint(o.w), NO_HIT);
+                else A.st.occ[kind * N + slot] = 0;
+                if (COUNT) {
+                    n_ext += kind == RK_EXT ? 1u : 0u;
+                    n_sh += kind == RK_EXT ? 0u : 1u;
+                }
             }
-        } else {
-            A.st.occ[kind * N + slot] = hit ? 1 : 0;
-            if (COUNT) ++n_sh;
+        }
+        if (__ballot(busy) == 0) break;
+        if (busy && trav_step<COUNT>(S, r, t, sc, stn, blockDim.x, cnt, nullptr, 0)) {
+            busy = false;
+            const bool hit = t.bestG != NO_HIT;
+            if (kind == RK_EXT) {
+                A.st.hit[slot] = make_uint2(__float_as_uint(t.bestT), t.bestG);
+                if (COUNT) {
+                    ++n_ext;
+                    n_hit += hit ? 1u : 0u;
+                }
+            } else {
+                A.st.occ[kind * N + slot] = hit ? 1 : 0;
+                if (COUNT) ++n_sh;
+            }
         }
     }
     if (COUNT) {

@@ -3,6 +3,7 @@
 #include "bvh_build.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -184,8 +185,11 @@ struct Builder {
     BuiltBVH& out;
     std::vector<uint32_t> order;
 
-    static constexpr int kBins = 16;
-    static constexpr uint32_t kLeafTarget = 4;
+    static constexpr int kMaxBins = 64;
+    int kBins = 16;             // NART_BVH_BINS (<= 64)
+    uint32_t kLeafTarget = 4;   // NART_BVH_LEAF: always a leaf at or below this many triangles
+    uint32_t kLeafSah = 8;      // NART_BVH_LEAF_SAH: SAH may stop splitting at or below this
+    float kTrav = 1.0f;         // NART_BVH_TRAV: node-visit cost relative to one triangle test
 
     int32_t make_leaf(uint32_t first, uint32_t count) {
         uint32_t leaf_first = (uint32_t)order.size();
@@ -209,16 +213,16 @@ struct Builder {
         for (int a = 0; a < 3; ++a) {
             float ext = cb.hi[a] - cb.lo[a];
             if (!(ext > 0.f)) continue;
-            Box bb[kBins];
-            uint32_t bc[kBins] = {0};
+            Box bb[kMaxBins];
+            uint32_t bc[kMaxBins] = {0};
             for (uint32_t i = first; i < first + count; ++i) {
                 int b = (int)((tris[i].c[a] - cb.lo[a]) / ext * kBins);
                 b = std::min(std::max(b, 0), kBins - 1);
                 bb[b].grow(tris[i].lo, tris[i].hi);
                 bc[b]++;
             }
-            Box lb[kBins];
-            uint32_t lc[kBins];
+            Box lb[kMaxBins];
+            uint32_t lc[kMaxBins];
             Box acc;
             uint32_t n = 0;
             for (int b = 0; b < kBins; ++b) {
@@ -244,7 +248,7 @@ struct Builder {
         }
         float leaf_cost = total.area() * count;
         bool force_split = count > NART_LEAF_MAX;
-        if (axis < 0 || (!force_split && best * 1.0f + total.area() * 1.0f >= leaf_cost * 1.0f && count <= 8)) {
+        if (axis < 0 || (!force_split && best + total.area() * kTrav >= leaf_cost && count <= kLeafSah)) {
             if (!force_split) return make_leaf(first, count);
         }
         uint32_t mid;
@@ -301,6 +305,10 @@ void build_bvh(const nart_scene_blob& blob, const std::vector<uint8_t>& mask, fl
     out.max_stack = 1;
     out.pad = pad;
     Builder bld{blob, tris, pad, out, {}};
+    if (const char* e = std::getenv("NART_BVH_BINS")) bld.kBins = std::max(2, std::min(Builder::kMaxBins, std::atoi(e)));
+    if (const char* e = std::getenv("NART_BVH_LEAF")) bld.kLeafTarget = (uint32_t)std::max(1, std::min(NART_LEAF_MAX, std::atoi(e)));
+    if (const char* e = std::getenv("NART_BVH_LEAF_SAH")) bld.kLeafSah = (uint32_t)std::max(1, std::min(NART_LEAF_MAX, std::atoi(e)));
+    if (const char* e = std::getenv("NART_BVH_TRAV")) bld.kTrav = (float)std::atof(e);
     if (tris.empty()) {
         out.root_code = -1;  // never traversed (geometry_visible = 0)
         out.num_leaf_tris = 0;
@@ -308,6 +316,26 @@ void build_bvh(const nart_scene_blob& blob, const std::vector<uint8_t>& mask, fl
     }
     out.root_code = bld.build(0, (uint32_t)tris.size(), 0);
     out.num_leaf_tris = (uint32_t)bld.order.size();
+    // Breadth-first node order: any prefix of the array is the top of the tree, which the
+    // traversal kernels keep in LDS (as much as fits).
+    if (out.root_code >= 0) {
+        std::vector<int32_t> bfs, remap(out.nodes.size(), -1);
+        bfs.push_back(out.root_code);
+        for (size_t h = 0; h < bfs.size(); ++h) {
+            const nd::BVHNode& n = out.nodes[bfs[h]];
+            for (int c = 0; c < 2; ++c)
+                if (n.child[c] >= 0) bfs.push_back(n.child[c]);
+        }
+        for (size_t i = 0; i < bfs.size(); ++i) remap[bfs[i]] = (int32_t)i;
+        std::vector<nd::BVHNode> reordered(bfs.size());
+        for (size_t i = 0; i < bfs.size(); ++i) {
+            reordered[i] = out.nodes[bfs[i]];
+            for (int c = 0; c < 2; ++c)
+                if (reordered[i].child[c] >= 0) reordered[i].child[c] = remap[reordered[i].child[c]];
+        }
+        out.nodes.swap(reordered);
+        out.root_code = 0;
+    }
     out.tri_isect.resize(bld.order.size() * 16);
     for (size_t i = 0; i < bld.order.size(); ++i) {
         uint32_t g = bld.order[i];

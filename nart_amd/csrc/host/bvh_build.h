@@ -11,7 +11,7 @@
 namespace nart {
 
 struct BuiltBVH {
-    std::vector<nd::BVHNode> nodes;   // depth-first, root = nodes[0] unless root_code < 0
+    std::vector<nd::BVHNode> nodes;   // breadth-first, root = nodes[0] unless root_code < 0
     std::vector<float> tri_isect;      // 16 floats per triangle, leaf order
     int32_t root_code = 0;
     uint32_t max_stack = 1;            // deepest chain of inner nodes (traversal stack bound)

@@ -22,8 +22,10 @@ struct nart_ctx {
     std::string err;
     DScene scene;
     uint32_t stack_depth = 1;
+    uint32_t num_nodes = 0;
     int variant = 0;
     bool counters = false;
+    bool has_env = false;  // scene has an environment light (selects the k_render build)
     // scene buffers
     void* d_nodes = nullptr;
     void* d_tri_isect = nullptr;
@@ -281,18 +283,42 @@ int ensure(nart_ctx* ctx, size_t slots, uint32_t spp, size_t buckets) {
     return NART_OK;
 }
 
-template <int MAXL, bool COUNT>
+// LDS of one k_render block: traversal stack + as many top BVH nodes as fit while
+// NART_RENDER_WAVES blocks share a CU's 160 KiB (NART_LDS_NODES overrides the node count).
+uint32_t render_lds_nodes(const nart_ctx* ctx) {
+    const size_t stack = (size_t)ctx->stack_depth * 256 * 8;
+    const size_t budget = (size_t)160 * 1024 / NART_RENDER_WAVES;
+    size_t n = budget > stack ? (budget - stack) / sizeof(BVHNode) : 0;
+    if (const char* e = std::getenv("NART_LDS_NODES")) n = (size_t)std::strtoul(e, nullptr, 10);
+    return (uint32_t)std::min<size_t>(n, ctx->num_nodes);
+}
+
+template <int MAXL, bool COUNT, bool ENV>
 void launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
+    static bool attr = false;  // dynamic LDS above the 64 KiB default
+    if (!attr) {
+        hipFuncSetAttribute((const void*)k_render<MAXL, COUNT, ENV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+        attr = true;
+    }
+    RenderArgs b = a;
+    b.lds_nodes = render_lds_nodes(ctx);
     dim3 grid((a.n_slots + 255) / 256), block(256);
-    size_t lds = (size_t)ctx->stack_depth * 256 * 8;
-    hipLaunchKernelGGL((k_render<MAXL, COUNT>), grid, block, lds, st, ctx->scene, a);
+    size_t lds = (size_t)ctx->stack_depth * 256 * 8 + (size_t)b.lds_nodes * sizeof(BVHNode);
+    hipLaunchKernelGGL((k_render<MAXL, COUNT, ENV>), grid, block, lds, st, ctx->scene, b);
+}
+
+template <bool ENV>
+void launch_render_maxl(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
+    const bool c = ctx->counters;
+    if (a.bounces <= 10) c ? launch_render<10, true, ENV>(ctx, a, st) : launch_render<10, false, ENV>(ctx, a, st);
+    else if (a.bounces <= 16) c ? launch_render<16, true, ENV>(ctx, a, st) : launch_render<16, false, ENV>(ctx, a, st);
+    else c ? launch_render<32, true, ENV>(ctx, a, st) : launch_render<32, false, ENV>(ctx, a, st);
 }
 
 int dispatch_megakernel(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
-    const bool c = ctx->counters;
-    if (a.bounces <= 10) c ? launch_render<10, true>(ctx, a, st) : launch_render<10, false>(ctx, a, st);
-    else if (a.bounces <= 16) c ? launch_render<16, true>(ctx, a, st) : launch_render<16, false>(ctx, a, st);
-    else c ? launch_render<32, true>(ctx, a, st) : launch_render<32, false>(ctx, a, st);
+    if (ctx->has_env) launch_render_maxl<true>(ctx, a, st);
+    else launch_render_maxl<false>(ctx, a, st);
     HIPCHK(hipGetLastError());
     return NART_OK;
 }
@@ -498,6 +524,7 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         ra.H = p->image_height;
         ra.totalW = g.total_width;
         ra.stack_depth = ctx->stack_depth;
+        ra.lds_nodes = 0;
         ra.gamma = p->roughening_factor * p->roughening_factor;
         ra.counters = ctx->d_counters;
         HIPCHK(hipEventRecord(ctx->ev[3], st));
@@ -607,6 +634,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     nart::build_bvh(*blob, mask, maxabs * 6.103515625e-05f + 1e-6f, bvh);
     ctx->stack_depth = std::max<uint32_t>(bvh.max_stack + 1, 2);
     if ((rc = upload(ctx, ctx->d_nodes, bvh.nodes.data(), bvh.nodes.size()))) return bail(rc);
+    ctx->num_nodes = (uint32_t)bvh.nodes.size();
     if ((rc = upload(ctx, ctx->d_tri_isect, bvh.tri_isect.data(), bvh.tri_isect.size()))) return bail(rc);
     if ((rc = upload(ctx, ctx->d_tris, blob->triangles, blob->num_triangles))) return bail(rc);
     std::vector<uint32_t> tri_mesh(blob->num_triangles);
@@ -638,6 +666,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     for (uint32_t l = 0; l < blob->num_lights; ++l) {
         lights.push_back(dlight(blob->lights[l]));
         const nart_light& L = blob->lights[l];
+        if (L.type == NART_LIGHT_ENVIRONMENT) ctx->has_env = true;
         if (L.type == NART_LIGHT_ENVIRONMENT && L.Le.type == NART_PTN_TEXTURE) {
             DEnvDist d;
             if ((rc = build_env(ctx, blob->textures[L.Le.texture], d))) return bail(rc);
@@ -810,6 +839,7 @@ int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t
     ra.H = p->image_height;
     ra.totalW = g.total_width;
     ra.stack_depth = ctx->stack_depth;
+    ra.lds_nodes = 0;
     ra.gamma = p->roughening_factor * p->roughening_factor;
     ra.counters = ctx->d_counters;
     rc = launch_latin(ctx, ra, 0);
