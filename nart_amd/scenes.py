@@ -3,6 +3,7 @@
     glassSphere  the reference's input/scenes/glassSphere.json with sphere.geo and backdrop.geo,
                  unpacked from assets/glassSphere.npz (packed by tools/pack_assets.py because
                  /root/reference is not present on the GPU box).  C1 / C3 of BASELINE.json.
+    ring, veach  the reference's ring.json (three sessions) and veach.json, packed the same way.
     cornell      a synthesized Lambert-only Cornell box lit by one disk light (C2 of
                  BASELINE.json; the reference ships no Cornell box).  Walls are 8x8-quad
                  grids and two boxes, so the reference octree gets many chunks (Q14).
@@ -56,22 +57,31 @@ def write_geo(path, faces, verts, normals, face_normals, uvs=None, face_uvs=None
         f.write(" ".join(toks) + "\n")
 
 
-def glass_sphere(directory=None):
-    """Unpack glassSphere into `directory`; returns the JSON path."""
-    d = directory or tempfile.mkdtemp(prefix="nart_glassSphere_")
+REFERENCE_SCENES = ("glassSphere", "ring", "veach")
+
+
+def reference_scene(name, directory=None):
+    """Materialise a packed reference scene (assets/<name>.npz, tools/pack_assets.py) into
+    `directory`; returns the JSON path."""
+    d = directory or tempfile.mkdtemp(prefix="nart_%s_" % name)
     os.makedirs(d, exist_ok=True)
-    z = np.load(os.path.join(ASSETS, "glassSphere.npz"), allow_pickle=False)
+    z = np.load(os.path.join(ASSETS, name + ".npz"), allow_pickle=False)
     scene = json.loads(bytes(z["scene_json"]).decode())
     for m in scene["meshes"]:
-        name = m["filePath"]
-        p = os.path.join(d, name)
+        fname = m["filePath"]
+        p = os.path.join(d, fname)
         if not os.path.exists(p):
-            _write_geo(p, z["geo_" + name + "_kinds"], z["geo_" + name + "_ints"], z["geo_" + name + "_floats"])
+            _write_geo(p, z["geo_" + fname + "_kinds"], z["geo_" + fname + "_ints"], z["geo_" + fname + "_floats"])
         m["filePath"] = p
-    path = os.path.join(d, "glassSphere.json")
+    path = os.path.join(d, name + ".json")
     with open(path, "w") as f:
         json.dump(scene, f, indent=1)
     return path
+
+
+def glass_sphere(directory=None):
+    """glassSphere (C1 / C3 of BASELINE.json); returns the JSON path."""
+    return reference_scene("glassSphere", directory)
 
 
 def _grid_quad(origin, u, v, n, res):

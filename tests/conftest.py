@@ -66,6 +66,14 @@ def volume_scenes(built, tmp_path_factory):
 
 
 @pytest.fixture(scope="session")
+def ref_scenes(built, tmp_path_factory):
+    """Reference scenes packed in assets/ (ring: ring light + 3 sessions; veach: 4 disk lights)."""
+    import nart_amd
+    from nart_amd import scenes
+    return {n: nart_amd.Scene(scenes.reference_scene(n, str(tmp_path_factory.mktemp(n)))) for n in ("ring", "veach")}
+
+
+@pytest.fixture(scope="session")
 def gpu(built):
     import torch
     assert torch.cuda.is_available(), "GPU tests need a visible MI355X"

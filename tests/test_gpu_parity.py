@@ -161,6 +161,21 @@ def test_volume_per_sample(gpu, volume_scenes):
     assert _bits_equal(g, r), _report(g, r)
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("name", ["ring", "veach"])
+def test_reference_scenes_all_sessions(gpu, ref_scenes, name, variant):
+    """The reference's own ring.json (every session: roughening 0 / 0.2 / 0.3) and veach.json
+    (MIS over four disk lights of different radii, plastic plates with eta 8192)."""
+    sc = ref_scenes[name]
+    r = nart_amd.HipRenderer(sc, variant=variant)
+    o = oracle.Oracle(sc)
+    for p in nart_amd.load_sessions(sc.path):
+        p.image_width, p.image_height, p.spp = 128, 72, 4
+        g = r.render(p)
+        ref = o.render(p)
+        assert _bits_equal(g, ref), _report(g, ref)
+
+
 @pytest.mark.parametrize("bounces", [0, 1, 2, 12, 20])
 def test_bounce_limits(glass_gpu, glass_oracle, glass_scene, bounces):
     """Bounce caps (pathintegrator.cpp:165): none, shallow, and the 16/32-entry list builds."""

@@ -170,3 +170,31 @@ def test_materials_scene_ingests(built, tmp_path):
     sc = nart_amd.Scene(scenes.materials(str(tmp_path)))
     c = sc.counts()
     assert c["materials"] == 7 and c["lights"] == 2 and c["textures"] >= 3
+
+
+REF = "/root/reference"
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "input", "scenes")), reason="reference checkout not present")
+@pytest.mark.parametrize("name", ["glassSphere", "ring", "veach"])
+def test_packed_reference_scene_equals_original(built, tmp_path, name):
+    """assets/<name>.npz materialises to a scene that renders bit-identically (oracle, every
+    session) to the reference's own input/scenes/<name>.json loaded from its checkout."""
+    import numpy as np
+    import nart_amd
+    import oracle
+    from nart_amd import scenes
+    packed = nart_amd.Scene(scenes.reference_scene(name, str(tmp_path)))
+    cwd = os.getcwd()
+    os.chdir(REF)  # the reference's paths are relative to its root ("input//meshes//...")
+    try:
+        orig = nart_amd.Scene(os.path.join("input", "scenes", name + ".json"))
+        sessions = nart_amd.load_sessions(os.path.join("input", "scenes", name + ".json"))
+    finally:
+        os.chdir(cwd)
+    assert packed.counts() == orig.counts()
+    for p in sessions:
+        p.image_width, p.image_height, p.spp = 40, 24, 2
+        a = oracle.Oracle(packed).render(p)
+        b = oracle.Oracle(orig).render(p)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))

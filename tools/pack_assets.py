@@ -1,5 +1,7 @@
-"""Pack the reference's glassSphere scene (input/scenes/glassSphere.json + the two .geo meshes it
-uses) into assets/glassSphere.npz, because /root/reference does not exist on the GPU box.
+"""Pack reference scenes (input/scenes/<name>.json + the .geo meshes they use) into
+assets/<name>.npz, because /root/reference does not exist on the GPU box: glassSphere (C1/C3),
+ring (ring light, three sessions) and veach (four disk lights of different sizes over plastic
+plates, the MIS test scene).
 
 Numbers are stored as values, not text: .geo floats are parsed with the C library's strtof
 (what `std::istream >> float` does in LoadMeshFromFile, scene.cpp:132-139) and JSON numbers as
@@ -34,8 +36,8 @@ def parse_geo(path):
     return (np.array(kinds, np.uint8), np.array(ints, np.uint32), np.array(floats, np.float32))
 
 
-def main(ref):
-    scene_path = os.path.join(ref, "input", "scenes", "glassSphere.json")
+def main(ref, scene_name="glassSphere"):
+    scene_path = os.path.join(ref, "input", "scenes", scene_name + ".json")
     scene = json.load(open(scene_path))
     arrays = {}
     for m in scene["meshes"]:
@@ -48,10 +50,12 @@ def main(ref):
             arrays["geo_" + name + "_floats"] = f
         m["filePath"] = name
     arrays["scene_json"] = np.frombuffer(json.dumps(scene).encode(), np.uint8)
-    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets", "glassSphere.npz")
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets", scene_name + ".npz")
     np.savez_compressed(out, **arrays)
     print("wrote", out, os.path.getsize(out), "bytes")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "/root/reference")
+    ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+    for name in (sys.argv[2:] or ["glassSphere"]):
+        main(ref, name)
