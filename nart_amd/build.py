@@ -49,10 +49,12 @@ def _sources(*rel):
 def build_scene_lib(force=False):
     os.makedirs(LIB, exist_ok=True)
     out = os.path.join(LIB, "libnart_scene.so")
-    srcs = _sources("host/scene_host.cpp", "host/json.h") + [os.path.join(REPO, "include", "nart_scene.h")]
+    srcs = _sources("host/scene_host.cpp", "host/json.h", "host/exr_piz.cpp", "host/exr_piz.h") + \
+        [os.path.join(REPO, "include", "nart_scene.h")]
     if not force and _newer(out, srcs):
         return out
-    _run(["g++"] + COMMON + ["-shared", "-o", out, os.path.join(CSRC, "host", "scene_host.cpp"), "-lz"])
+    _run(["g++"] + COMMON + ["-shared", "-o", out, os.path.join(CSRC, "host", "scene_host.cpp"),
+                             os.path.join(CSRC, "host", "exr_piz.cpp"), "-lz"])
     return out
 
 

@@ -23,6 +23,7 @@
 #include <zlib.h>
 
 #include "../../../include/nart_scene.h"
+#include "exr_piz.h"
 #include "json.h"
 
 namespace {
@@ -910,7 +911,7 @@ int nart_write_exr(const char* path, const nart_render_params* p, const nart_pix
     return wr == f.size() ? NART_OK : set_error(NART_E_IO, "short write");
 }
 
-// RgbaInputFile-style reader: scanline files, NONE / RLE / ZIPS / ZIP, HALF or FLOAT channels,
+// RgbaInputFile-style reader: scanline files, NONE / RLE / ZIPS / ZIP / PIZ, HALF or FLOAT channels,
 // R/G/B/A or Y (luminance -> gray).  Returns halves, row 0 = first scanline of the data window.
 int nart_read_exr_rgba(const char* path, uint32_t* width, uint32_t* height, uint16_t** rgba) {
     std::string s;
@@ -955,7 +956,8 @@ int nart_read_exr_rgba(const char* path, uint32_t* width, uint32_t* height, uint
     switch (compression) {
         case 0: case 1: case 2: lpc = 1; break;
         case 3: lpc = 16; break;
-        default: return set_error(NART_E_UNSUPPORTED, std::string("EXR compression ") + std::to_string(compression) + " not supported (PIZ/PXR24/B44/DWA)");
+        case 4: lpc = 32; break;  // PIZ (exr_piz.cpp)
+        default: return set_error(NART_E_UNSUPPORTED, std::string("EXR compression ") + std::to_string(compression) + " not supported (PXR24/B44/DWA)");
     }
     size_t bpp_line = 0;
     for (auto& c : chans) bpp_line += (c.type == 1 ? 2 : 4) * size_t(W);
@@ -976,6 +978,11 @@ int nart_read_exr_rgba(const char* path, uint32_t* width, uint32_t* height, uint
         const uint8_t* src = b + off + 8;
         if (dsz == rawsz) {
             std::memcpy(raw.data(), src, rawsz);
+        } else if (compression == 4) {
+            std::vector<int> types;
+            for (auto& c : chans) types.push_back(c.type);
+            if (!nart::piz_decode(src, dsz, types.data(), int(types.size()), W, lines, raw) || raw.size() != rawsz)
+                return set_error(NART_E_INVALID, "PIZ chunk decode failed");
         } else if (compression == 1) {
             std::vector<uint8_t> t;
             size_t q = 0;

@@ -198,3 +198,25 @@ def test_packed_reference_scene_equals_original(built, tmp_path, name):
         a = oracle.Oracle(packed).render(p)
         b = oracle.Oracle(orig).render(p)
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "input", "textures")), reason="reference checkout not present")
+@pytest.mark.parametrize("rel,shape", [("glassIceWater/iceCube_normal.exr", (512, 512)),
+                                       ("glassIceWater/iceCube_roughness.exr", (512, 512)),
+                                       ("glassIceWater/glass_roughness.exr", (4096, 4096)),
+                                       ("cameraLens/lens_roughness.exr", (4096, 4096))])
+def test_piz_textures_decode(built, rel, shape):
+    """PIZ (wavelet + Huffman) textures the reference ships (HALF BGR, HALF Y, FLOAT Y): every
+    chunk's Huffman stream must decode to exactly the chunk's sample count (the decoder rejects
+    anything else), values are finite, in the texture's [0, 1] range and spatially smooth (a
+    wrong wavelet or LUT step yields noise).  No PIZ encoder or OpenEXR is available here, so
+    the texel values themselves are unpinned."""
+    import numpy as np
+    import nart_amd
+    a = nart_amd.read_exr(os.path.join(REF, "input", "textures", rel))
+    assert a.shape == shape + (4,)
+    rgb = a[..., :3]
+    assert np.isfinite(rgb).all() and rgb.min() >= 0.0 and rgb.max() <= 1.0
+    assert np.all(a[..., 3] == 1.0)  # no alpha channel -> 1
+    dx = np.abs(np.diff(rgb, axis=1)).mean()
+    assert dx < 0.1 * (rgb.max() - rgb.min())
