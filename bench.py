@@ -1,6 +1,6 @@
 """Bench: Msamples/s of nart's render path on glassSphere.json at 1920x1080, 256 spp (C3).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
 A step renders the whole frame once: every rank renders an interleaved share of the
@@ -10,10 +10,13 @@ so the image is bit-identical for any N.  Total work is fixed as N grows ("stron
 
 value = W*H*spp*K / T (Msamples/s, camera samples, render.cpp:164-168 extra rows excluded),
 T = max over ranks of the barrier-bracketed wall time of the K steps.
-roofline: the path-tracing kernel's algorithmic bytes per launch (counter pass: BVH node and
-triangle records, winner attributes, per-sample I/O) / its HIP-event duration.
+roofline: the path-tracing kernel's algorithmic bytes per launch (counter pass, SURVEY.md 8(d)
+per-sample figure) / its HIP-event duration.
 cpu_baseline: the oracle (line-faithful C restatement of the TBB tile renderer, oracle/) on a
-bounded bucket sample of the same frame, timed on this host (rank 0, N=1 only).
+bounded bucket sample of the same frame, timed on this host (rank 0, N=1 only).  The GPU's
+tiles of those buckets are compared with the oracle's bit for bit ("parity").
+The other BASELINE.json configs (C2 Cornell, C4 environment-lit textured scene, C5 volume) run
+with --config; the default (C3) is the metric BASELINE.json names.
 """
 import argparse
 import json
@@ -31,8 +34,22 @@ import nart_amd  # noqa: E402
 from nart_amd import scenes  # noqa: E402
 from nart_amd.dist import BucketShard  # noqa: E402
 
-WIDTH, HEIGHT, SPP = 1920, 1080, 256
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md, chip-level parameters)
+
+CONFIGS = {
+    "c3": dict(scene=lambda d: scenes.glass_sphere(d), w=1920, h=1080, spp=256, stride=29,
+               workload="C3 glassSphere.json 1920x1080 256spp, bucket 16, bounces 10, filterWidth 2, roughening 0.2",
+               data="reference scene input/scenes/glassSphere.json (+ sphere.geo, backdrop.geo) packed in assets/"),
+    "c2": dict(scene=lambda d: scenes.cornell(d), w=1920, h=1080, spp=64, stride=29,
+               workload="C2 synthesized Lambert Cornell box, one disk light, 1920x1080 64spp, bounces 10",
+               data="synthesized scene (nart_amd/scenes.py cornell)"),
+    "c4": dict(scene=lambda d: scenes.environment(d), w=3840, h=2160, spp=512, stride=211,
+               workload="C4-style environment-lit textured, normal-mapped plastic + rough glass, 3840x2160 512spp",
+               data="synthesized scene + generated sky EXR (nart_amd/scenes.py environment)"),
+    "c5": dict(scene=lambda d: scenes.volume(d, kind="c5"), w=1920, h=1080, spp=1024, stride=59,
+               workload="C5 homogeneous medium (density 1, sigma_s 8), volume integrator, 1920x1080 1024spp, 32 bounces",
+               data="synthesized .vol + generated sky EXR (nart_amd/scenes.py volume)"),
+}
 
 
 def bytes_per_sample(c):
@@ -46,17 +63,23 @@ def bytes_per_sample(c):
             + 256.0 * c["bounces"]) / n + 40.0
 
 
-def cpu_baseline(scene, p):
+def cpu_sample_ids(p, stride):
+    g = nart_amd.session_geometry(p)
+    nb = g.n_buckets_x * g.n_buckets_y
+    stride = int(os.environ.get("NART_CPU_BUCKET_STRIDE", str(stride)))
+    return np.arange(0, nb, stride, dtype=np.uint32), stride
+
+
+def cpu_baseline(scene, p, ids, stride):
+    """Oracle on the sampled buckets (timed), returning the rate and the oracle's tiles."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
     g = nart_amd.session_geometry(p)
     nb = g.n_buckets_x * g.n_buckets_y
-    stride = int(os.environ.get("NART_CPU_BUCKET_STRIDE", "29"))
-    ids = np.arange(0, nb, stride, dtype=np.uint32)
     threads = oracle.default_threads()
     orc = oracle.Oracle(scene)
     t = time.time()
-    orc.render_buckets(p, ids, threads)
+    tiles = orc.render_buckets(p, ids, threads)
     dt = time.time() - t
     samples = 0
     for i in ids:
@@ -64,19 +87,21 @@ def cpu_baseline(scene, p):
         x1 = min(p.bucket_size * (bx + 1), p.image_width)
         y1 = min(p.bucket_size * (by + 1), p.image_height)
         samples += max(0, x1 - p.bucket_size * bx) * max(0, y1 - p.bucket_size * by) * p.spp
-    return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": "%d of %d buckets (every %dth in raster order, 29 coprime to the 120 bucket columns) of the same %dx%d %dspp frame, %d samples, %.1f s"
-                      % (len(ids), nb, stride, p.image_width, p.image_height, p.spp, samples, dt)}
+    out = {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+           "sample": "%d of %d buckets (every %dth in raster order, coprime to the %d bucket columns) of the same "
+                     "%dx%d %dspp frame, %d samples, %.1f s" % (len(ids), nb, stride, g.n_buckets_x, p.image_width,
+                                                              p.image_height, p.spp, samples, dt)}
+    return out, tiles
 
 
-def load_traffic(kernel_avg_ms):
+def load_traffic(tag):
     """HBM bytes per launch of the render kernel from the committed rocprofv3 PMC summary."""
     path = os.path.join(REPO, "profiles", "pmc_latest.json")
     if not os.path.exists(path):
         return None
     try:
         d = json.load(open(path))
-        if d.get("config") == "%dx%dx%d" % (WIDTH, HEIGHT, SPP):
+        if d.get("config") == tag:
             return d.get("hbm_bytes_per_launch")
     except Exception:
         return None
@@ -88,8 +113,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     a = ap.parse_args()
+    cfg = CONFIGS[a.config]
+    W, H, SPP = cfg["w"], cfg["h"], cfg["spp"]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -100,11 +128,11 @@ def main():
         import torch.distributed as td
         td.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    scene_dir = os.path.join("/tmp", "nart_bench_scene_%d" % os.getpid())
-    path = scenes.glass_sphere(scene_dir)
+    scene_dir = os.path.join("/tmp", "nart_bench_scene_%s_%d" % (a.config, os.getpid()))
+    path = cfg["scene"](scene_dir)
     scene = nart_amd.Scene(path)
     p = nart_amd.load_sessions(path)[0]
-    p.image_width, p.image_height, p.spp = WIDTH, HEIGHT, SPP
+    p.image_width, p.image_height, p.spp = W, H, SPP
     g = nart_amd.session_geometry(p)
     nb = g.n_buckets_x * g.n_buckets_y
     tpx = g.tile_size * g.tile_size
@@ -113,10 +141,12 @@ def main():
     dev = torch.device("cuda", local)
     shard = BucketShard(nb, tpx, rank, world, dev)  # interleaved buckets, gather to rank 0
     mine = shard.mine
+    by_id = None
     if rank == 0:
         image = torch.zeros((g.total_height, g.total_width, 5), dtype=torch.float32, device=dev)
 
     def step(stats):
+        nonlocal by_id
         gpu.render_buckets_async(p, mine, shard.tiles.data_ptr(), stream.cuda_stream, stats)
         by_id = shard.gather()
         if rank == 0:
@@ -154,7 +184,7 @@ def main():
         td.all_reduce(tt, op=td.ReduceOp.MAX)
         dt = float(tt.item())
 
-    samples_total = WIDTH * HEIGHT * SPP * a.steps
+    samples_total = W * H * SPP * a.steps
     value = samples_total / dt / 1e6
     kernel_avg_ms = st.kernel_ms / max(1, st.kernel_launches)
     bps = bytes_per_sample(counters)
@@ -162,8 +192,9 @@ def main():
     achieved = bps * per_launch_samples / (kernel_avg_ms * 1e-3) / 1e9
     if rank == 0:
         img_ok = bool(torch.isfinite(image).all().item())
+        volume = p.integrator == 1
         out = {
-            "metric": "Msamples/s at 1920x1080x256spp (glassSphere.json)",
+            "metric": "Msamples/s at %dx%dx%dspp (%s)" % (W, H, SPP, os.path.basename(path)),
             "value": round(value, 3),
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -174,14 +205,14 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "reference scene input/scenes/glassSphere.json (+ sphere.geo, backdrop.geo) packed in assets/",
-            "config": {"workload": "C3 glassSphere.json 1920x1080 256spp, bucket 16, bounces 10, filterWidth 2, "
-                                   "roughening 0.2", "image": [WIDTH, HEIGHT], "spp": SPP, "buckets": nb,
+            "data": cfg["data"],
+            "config": {"workload": cfg["workload"], "image": [W, H], "spp": SPP, "buckets": nb,
                        "parallelism": "buckets interleaved over %d rank(s), RCCL gather to rank 0" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": load_traffic(kernel_avg_ms),
-                         "kernel": "k_render", "kernel_avg_ms": round(kernel_avg_ms, 3),
-                         "bytes_per_sample": round(bps, 1)},
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "traffic": load_traffic("%dx%dx%d" % (W, H, SPP)),
+                         "kernel": "k_render_volume" if volume else "k_render",
+                         "kernel_avg_ms": round(kernel_avg_ms, 3), "bytes_per_sample": round(bps, 1)},
             "kernel_ms_per_step": round(st.kernel_ms / a.steps, 3),
             "splat_ms_per_step": round(st.splat_ms / a.steps, 3),
             "latin_ms_per_step": round(st.latin_ms / a.steps, 3),
@@ -191,8 +222,14 @@ def main():
                                               "bounces")},
         }
         if world == 1 and not a.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(scene, p)
+            ids, stride = cpu_sample_ids(p, cfg["stride"])
+            out["cpu_baseline"], ref_tiles = cpu_baseline(scene, p, ids, stride)
             out["vs_cpu_baseline"] = round(value / out["cpu_baseline"]["value"], 1)
+            gt = by_id[torch.from_numpy(ids.astype(np.int64)).to(dev)].cpu().numpy()
+            diff = np.abs(gt.astype(np.float64) - ref_tiles.astype(np.float64))
+            out["parity"] = {"buckets_compared": int(len(ids)), "tile_floats": int(gt.size),
+                             "bit_identical": bool(np.array_equal(gt.view(np.uint32), ref_tiles.view(np.uint32))),
+                             "max_abs_diff": float(diff.max()), "rmse": float(np.sqrt((diff ** 2).mean()))}
         print(json.dumps(out), flush=True)
     if dist:
         import torch.distributed as td

@@ -91,7 +91,15 @@ struct Trav {
 
 ND void trav_begin(const DScene& S, const Ray& r, float tmax, bool ANY, Trav& t) {
     // Box tests need not be exact (boxes are padded on the host), so use fast reciprocals.
-    t.inv = F3(__builtin_amdgcn_rcpf(r.d.x), __builtin_amdgcn_rcpf(r.d.y), __builtin_amdgcn_rcpf(r.d.z));
+    // They are clamped to +-1e20: for a zero direction component 1/d = inf would make
+    // fma(lo, inv, -o * inv) = inf - inf = NaN and reject a box the ray runs inside (a camera
+    // ray of the C3 frame has d.z == 0 exactly).  With the clamp the slab distances keep their
+    // signs and stay far beyond any scene distance unless the origin lies within float rounding
+    // of a padded face -- where the box holds no triangle the ray can reach.
+    const float BIG = 1e20f;
+    t.inv = F3(fminf(fmaxf(__builtin_amdgcn_rcpf(r.d.x), -BIG), BIG),
+               fminf(fmaxf(__builtin_amdgcn_rcpf(r.d.y), -BIG), BIG),
+               fminf(fmaxf(__builtin_amdgcn_rcpf(r.d.z), -BIG), BIG));
     t.oi = F3(-r.o.x * t.inv.x, -r.o.y * t.inv.y, -r.o.z * t.inv.z);
     t.tmax = tmax;
     t.bestT = tmax;

@@ -1823,3 +1823,52 @@ void oracle_latin_square(uint32_t seed, uint32_t spp, float* out_xy, uint32_t* s
 }
 
 float oracle_fresnel(float eta_o, float eta_i, float c) { return fresnel(eta_o, eta_i, c); }
+
+/* ---------------------------------------------------------------- debugging aids (tests/tools only) */
+/* Camera ray of pixel (x, y) with image sample (u, v) (pinholecamera.cpp:9-40). */
+void oracle_camera_ray(const oracle_scene* s, uint32_t W, uint32_t H, uint32_t x, uint32_t y, float u, float v,
+                       float* o, float* d) {
+    ray_t r = cast_ray(s, V2(u, v), W, H, x, y);
+    o[0] = r.o.x; o[1] = r.o.y; o[2] = r.o.z;
+    d[0] = r.d.x; d[1] = r.d.y; d[2] = r.d.z;
+}
+/* Closest hit of one ray: the reference octree (out[0] = triangle or -1, out[1] = t bits) and a
+   brute-force pass over every triangle with Triangle::Intersect, keeping the strictly closest
+   (out[2], out[3]).  tmax presets Intersection::tMax as the light loop does. */
+void oracle_trace(const oracle_scene* s, const float* o, const float* d, float tmax, int32_t* out) {
+    ray_t r = make_ray(V3(o[0], o[1], o[2]), V3(d[0], d[1], d[2]));
+    heap_t q = {0, 0, 0};
+    isect_t is;
+    isect_init(&is);
+    is.tMax = tmax;
+    int32_t best = -1;
+    if (bvh_intersect(s, &r, &is, &q)) {
+        /* find which triangle produced is.tMax */
+        for (uint32_t g = 0; g < s->blob->num_triangles; ++g) {
+            isect_t t1;
+            isect_init(&t1);
+            if (triangle_intersect(&s->blob->triangles[g], &r, &t1) && memcmp(&t1.tMax, &is.tMax, 4) == 0) {
+                best = (int32_t)g;
+                break;
+            }
+        }
+    }
+    free(q.e);
+    out[0] = best;
+    memcpy(&out[1], &is.tMax, 4);
+    isect_t bf;
+    isect_init(&bf);
+    bf.tMax = tmax;
+    int32_t bg = -1;
+    for (uint32_t g = 0; g < s->blob->num_triangles; ++g) {
+        isect_t t1;
+        isect_init(&t1);
+        t1.tMax = bf.tMax;
+        if (triangle_intersect(&s->blob->triangles[g], &r, &t1)) {
+            bf.tMax = t1.tMax;
+            bg = (int32_t)g;
+        }
+    }
+    out[2] = bg;
+    memcpy(&out[3], &bf.tMax, 4);
+}

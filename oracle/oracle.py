@@ -41,6 +41,9 @@ def lib():
         _lib.oracle_latin_square.argtypes = [ctypes.c_uint32, ctypes.c_uint32, P, P]
         _lib.oracle_fresnel.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_float]
         _lib.oracle_fresnel.restype = ctypes.c_float
+        _lib.oracle_camera_ray.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.c_float, ctypes.c_float, P, P]
+        _lib.oracle_trace.argtypes = [P, P, P, ctypes.c_float, P]
     return _lib
 
 
@@ -111,3 +114,22 @@ def latin_square(seed, spp):
 
 def fresnel(eta_o, eta_i, c):
     return lib().oracle_fresnel(eta_o, eta_i, c)
+
+
+def camera_ray(orc, W, H, x, y, u, v):
+    """Debug aid: the oracle's camera ray for pixel (x, y), sample (u, v)."""
+    o = (ctypes.c_float * 3)()
+    d = (ctypes.c_float * 3)()
+    lib().oracle_camera_ray(orc._h, W, H, x, y, ctypes.c_float(u), ctypes.c_float(v), o, d)
+    return np.array(o[:], np.float32), np.array(d[:], np.float32)
+
+
+def trace(orc, o, d, tmax=float("inf")):
+    """Debug aid: (octree triangle, t, brute-force triangle, t) for one ray."""
+    o = np.ascontiguousarray(o, np.float32)
+    d = np.ascontiguousarray(d, np.float32)
+    out = (ctypes.c_int32 * 4)()
+    lib().oracle_trace(orc._h, o.ctypes.data, d.ctypes.data, ctypes.c_float(tmax), out)
+    t0 = np.array([out[1]], np.int32).view(np.float32)[0]
+    t1 = np.array([out[3]], np.int32).view(np.float32)[0]
+    return out[0], float(t0), out[2], float(t1)
