@@ -176,6 +176,19 @@ def test_reference_scenes_all_sessions(gpu, ref_scenes, name, variant):
         assert _bits_equal(g, ref), _report(g, ref)
 
 
+def test_zero_direction_component_ray(gpu, glass_scene):
+    """C3 pixel (1352, 136), sample 187 casts a camera ray with d.z == 0 exactly (found by the
+    bench's in-run parity check): the slab test must not turn 1/0 into NaN boxes."""
+    p = _params(glass_scene, 1920, 1080, 256)
+    o = oracle.Oracle(glass_scene)
+    _, uv = o.render_samples(p, 1352, 136, 1, 1, with_uv=True)
+    _, d = oracle.camera_ray(o, 1920, 1080, 1352, 136, float(uv[0, 0, 187, 0]), float(uv[0, 0, 187, 1]))
+    assert d[2] == 0.0
+    g = nart_amd.HipRenderer(glass_scene).render_samples(p, 1344, 128, 16, 16)
+    r = o.render_samples(p, 1344, 128, 16, 16)
+    assert _bits_equal(g, r), _report(g, r)
+
+
 @pytest.mark.parametrize("bounces", [0, 1, 2, 12, 20])
 def test_bounce_limits(glass_gpu, glass_oracle, glass_scene, bounces):
     """Bounce caps (pathintegrator.cpp:165): none, shallow, and the 16/32-entry list builds."""
