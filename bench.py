@@ -219,7 +219,7 @@ def main():
             "image_finite": img_ok,
             "counters_per_sample": {k: round(counters[k] / max(1, counters["traced_samples"]), 3)
                                     for k in ("rays_extend", "rays_shadow", "node_visits", "tri_tests",
-                                              "bounces")},
+                                              "bounces", "octree_checks", "octree_replays")},
         }
         if world == 1 and not a.no_cpu_baseline:
             ids, stride = cpu_sample_ids(p, cfg["stride"])

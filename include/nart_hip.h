@@ -39,6 +39,9 @@ typedef struct nart_render_stats {
      * hits shaded (BSDF + EstimateDirect + continuation). */
     uint64_t rays_extend, rays_shadow, node_visits, tri_tests, bounces;
     double latin_ms;        /* device time of the LatinSquare kernel                    */
+    /* Counter pass only: hits whose octree reachability needed the exact ancestor-chain check,
+     * and queries answered by replaying the reference octree search (device/octree.h). */
+    uint64_t octree_checks, octree_replays;
 } nart_render_stats;
 
 /* Upload the scene, build the device BVH.  device_id: HIP ordinal. */

@@ -57,7 +57,8 @@ class RenderStats(ctypes.Structure):
                 ("kernel_launches", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("samples", ctypes.c_uint64),
                 ("traced_samples", ctypes.c_uint64), ("rays_extend", ctypes.c_uint64), ("rays_shadow", ctypes.c_uint64),
                 ("node_visits", ctypes.c_uint64), ("tri_tests", ctypes.c_uint64), ("bounces", ctypes.c_uint64),
-                ("latin_ms", ctypes.c_double)]
+                ("latin_ms", ctypes.c_double), ("octree_checks", ctypes.c_uint64),
+                ("octree_replays", ctypes.c_uint64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}

@@ -90,6 +90,20 @@ struct DMedium {
     const float* density;
 };
 
+// Reference octree (bvh.cpp:115-250), kept beside the device BVH so that the render path can
+// reproduce Octree::Intersect's reachability exactly (path.h, oc_resolve).  Node indices are
+// the reference's creation order; bmin/bmax are the BoundingVolume extents (axis dot products,
+// bvh.cpp:81-113, extended bottom-up as bvh.cpp:235-250).
+struct OcNode {
+    float bmin[3], bmax[3];
+    int32_t parent;        // -1 at the root
+    uint32_t chunk_first;  // leaves: first (tri_first, tri_count) pair in oc_chunks
+    uint32_t chunk_count;  // leaves: chunks in InsertChunk order; 0 for inner nodes
+    int32_t children[8];   // -1 where absent
+    int32_t is_leaf;
+};
+static_assert(sizeof(OcNode) == 72, "OcNode must be 72 B");
+
 struct DScene {
     const BVHNode* nodes;
     const float4* tri_isect;
@@ -108,6 +122,17 @@ struct DScene {
     float cam_m[16];
     float cam_tan;           // tan(radians(fov)) (host libm, as the reference)
     DMedium medium;
+    // reference octree + replay heap pool (oc_resolve in path.h)
+    const OcNode* oc_nodes;
+    const uint32_t* oc_chunks;  // (tri_first, tri_count) into oc_tris
+    const uint32_t* oc_tris;    // global triangle ids, chunk insertion order
+    const int32_t* tri_leaf;    // leaf node of each triangle, -1 if unreachable
+    uint32_t* oc_lock;          // [oc_pool] replay heap ownership
+    unsigned long long* oc_heap;// [oc_pool][oc_cap] (key bits | node << 32)
+    int32_t oc_root;
+    uint32_t oc_cap, oc_pool;
+    int32_t oc_exact;           // 0 disables the emulation (A/B only; not reference behaviour)
+    float oc_scale;             // max |coordinate| of the scene and camera (margins)
 };
 
 }  // namespace nd

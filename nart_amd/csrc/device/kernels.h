@@ -191,7 +191,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
     float* stn = s_tn + tid;
     const int stride = blockDim.x;
     const float nL = (float)S.num_lights;
-    TraceCounters cnt = {0u, 0u};
+    TraceCounters cnt = {0u, 0u, 0u, 0u};
     uint32_t n_ext = 0, n_sh = 0, n_bounce = 0;
 
     uint32_t s = 0;
@@ -410,6 +410,8 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
         atomicAdd(&A.counters[2], (unsigned long long)cnt.nodes);
         atomicAdd(&A.counters[3], (unsigned long long)cnt.tris);
         atomicAdd(&A.counters[4], (unsigned long long)n_bounce);
+        atomicAdd(&A.counters[5], (unsigned long long)cnt.oc_checks);
+        atomicAdd(&A.counters[6], (unsigned long long)cnt.oc_replays);
     }
 }
 

@@ -71,6 +71,7 @@ ND bool edges_accept(float e0, float e1, float e2) {  // geometry.cpp:78-81
 // ---------------------------------------------------------------- BVH traversal
 struct TraceCounters {
     uint32_t nodes, tris;
+    uint32_t oc_checks, oc_replays;  // octree.h: exact ancestor checks, octree replays
 };
 
 // Closest hit (ANY=false): minimum (t, scene index) over triangles with 0 < t < tmax whose
@@ -84,10 +85,19 @@ struct TraceCounters {
 struct Trav {
     f3 inv, oi;        // slab-test reciprocals and -o * inv
     float tmax, bestT;
+    float cullT;       // boxes entered beyond cullT are skipped (oc_cull(bestT); tmax for any-hit)
+    float t2;          // closest accepted hit other than the winner (or tmax)
     uint32_t bestG;
+    uint32_t bestInfo; // tri_isect word 14 of the winner: octree leaf | inside-leaf bit
     int code, sp;
-    bool any;
+    bool any, risky;   // risky: a NaN plane distance or an exact tie with the winner was seen
 };
+
+// Closest-hit culling distance.  Boxes are kept up to a little beyond the best hit so that every
+// hit within oc_cull(t*) of the winner is tested: then min(t2, oc_cull(t*)) bounds every other
+// hit from below, which octree.h needs (oc_resolve).  Monotone in b, so a box culled when the
+// best was b >= t* holds no hit below oc_cull(t*).
+ND float oc_cull(const DScene& S, float b) { return b + (b * 0x1p-12f + S.oc_scale * 0x1p-20f); }
 
 ND void trav_begin(const DScene& S, const Ray& r, float tmax, bool ANY, Trav& t) {
     // Box tests need not be exact (boxes are padded on the host), so use fast reciprocals.
@@ -103,10 +113,14 @@ ND void trav_begin(const DScene& S, const Ray& r, float tmax, bool ANY, Trav& t)
     t.oi = F3(-r.o.x * t.inv.x, -r.o.y * t.inv.y, -r.o.z * t.inv.z);
     t.tmax = tmax;
     t.bestT = tmax;
+    t.cullT = ANY ? tmax : oc_cull(S, tmax);
+    t.t2 = tmax;
     t.bestG = NO_HIT;
+    t.bestInfo = 0u;
     t.code = S.root;
     t.sp = 0;
     t.any = ANY;
+    t.risky = false;
 }
 
 // pop the next subtree that can still contain a closer hit
@@ -114,7 +128,7 @@ ND bool trav_pop(Trav& t, const int* sc, const float* st, int stride) {
     while (t.sp > 0) {
         --t.sp;
         const float tn = st[t.sp * stride];
-        if (tn <= t.bestT) {
+        if (tn <= t.cullT) {
             t.code = sc[t.sp * stride];
             return true;
         }
@@ -157,8 +171,8 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
         float uz0 = fmaf(c.x, inv.z, oi.z), uz1 = fmaf(c.w, inv.z, oi.z);
         float n1 = fmaxf(fmaxf(fminf(ux0, ux1), fminf(uy0, uy1)), fminf(uz0, uz1));
         float f1 = fminf(fminf(fmaxf(ux0, ux1), fmaxf(uy0, uy1)), fmaxf(uz0, uz1));
-        bool h0 = (n0 <= f0) && (f0 >= 0.f) && (n0 <= t.bestT);
-        bool h1 = (n1 <= f1) && (f1 >= 0.f) && (n1 <= t.bestT);
+        bool h0 = (n0 <= f0) && (f0 >= 0.f) && (n0 <= t.cullT);
+        bool h1 = (n1 <= f1) && (f1 >= 0.f) && (n1 <= t.cullT);
         if (h0 && h1) {
             bool swap = n1 < n0;
             sc[t.sp * stride] = swap ? k.x : k.y;
@@ -184,21 +198,39 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
         if (!edges_accept(e0, e1, e2)) continue;
         float4 a = tp[0];
         f3 n = F3(a.x, a.y, a.z);
-        float tt = (a.w - dot(r.o, n)) / dot(r.d, n);
+        const float den = dot(r.d, n);
+        float tt = (a.w - dot(r.o, n)) / den;
+        if (tt != tt) t.risky = true;                   // NaN passes geometry.cpp:37-39 (octree.h)
         if (!(tt > 0.f) || !(tt < t.tmax)) continue;  // geometry.cpp:37-39 with tMin = 0
         uint32_t g = __float_as_uint(dd.y);
+        const uint32_t info = __float_as_uint(dd.z) & (fabsf(den) >= dd.w ? 0xFFFFFFFFu : 0x7FFFFFFFu);
         if (t.any) {
             t.bestT = tt;
             t.bestG = g;
+            t.bestInfo = info;
             return true;
         }
-        if (tt < t.bestT || (tt == t.bestT && g < t.bestG)) {
+        if (tt < t.bestT) {
+            t.t2 = t.bestT;
             t.bestT = tt;
             t.bestG = g;
+            t.bestInfo = info;
+            t.cullT = oc_cull(S, tt);
+        } else {
+            if (tt == t.bestT) {
+                t.risky = true;  // the octree keeps the first chunk it visits, not the lowest index
+                t.bestInfo = g < t.bestG ? info : t.bestInfo;
+                t.bestG = g < t.bestG ? g : t.bestG;
+            }
+            t.t2 = fminf(t.t2, tt);
         }
     }
     return !trav_pop(t, sc, st, stride);
 }
+
+}  // namespace nd
+#include "octree.h"
+namespace nd {
 
 template <bool COUNT>
 ND bool traverse(const DScene& S, const Ray& r, float tmax, bool ANY, float& bestT, uint32_t& bestG, int* sc,
@@ -212,6 +244,7 @@ ND bool traverse(const DScene& S, const Ray& r, float tmax, bool ANY, float& bes
     }
     bestT = t.bestT;
     bestG = t.bestG;
+    oc_resolve<COUNT>(S, r, tmax, ANY, t.risky, t.bestInfo, fminf(t.t2, oc_cull(S, t.bestT)), bestT, bestG, cnt);
     return bestG != NO_HIT;
 }
 

@@ -173,7 +173,7 @@ __global__ __launch_bounds__(256) void k_wf_trace(DScene S, WFArgs A, uint32_t i
     const uint32_t n = ne + A.counts[2 + cur];
     const uint32_t gsize = gridDim.x * blockDim.x;
     const size_t N = A.R.n_slots;
-    TraceCounters cnt = {0u, 0u};
+    TraceCounters cnt = {0u, 0u, 0u, 0u};
     uint32_t n_ext = 0, n_sh = 0, n_hit = 0;
     // Persistent lanes with dynamic ray fetching: a lane whose ray is resolved takes its next
     // ray (grid-stride order) before the next traversal step, instead of idling until the
@@ -207,6 +207,7 @@ __global__ __launch_bounds__(256) void k_wf_trace(DScene S, WFArgs A, uint32_t i
         if (__ballot(busy) == 0) break;
         if (busy && trav_step<COUNT>(S, r, t, sc, stn, blockDim.x, cnt, nullptr, 0)) {
             busy = false;
+            oc_resolve<COUNT>(S, r, t.tmax, t.any, t.risky, t.bestInfo, fminf(t.t2, oc_cull(S, t.bestT)), t.bestT, t.bestG, cnt);
             const bool hit = t.bestG != NO_HIT;
             if (kind == RK_EXT) {
                 A.st.hit[slot] = make_uint2(__float_as_uint(t.bestT), t.bestG);
@@ -230,6 +231,8 @@ __global__ __launch_bounds__(256) void k_wf_trace(DScene S, WFArgs A, uint32_t i
             atomicAdd(&A.R.counters[3], (unsigned long long)tt);
             atomicAdd(&A.R.counters[4], (unsigned long long)hh);
         }
+        atomicAdd(&A.R.counters[5], (unsigned long long)cnt.oc_checks);
+        atomicAdd(&A.R.counters[6], (unsigned long long)cnt.oc_replays);
     }
 }
 

@@ -78,10 +78,95 @@ struct Octree {
     }
 };
 
+// glm::dot(v, axis) for the unit axes (bvh.cpp:95-100): (x*a.x + y*a.y) + z*a.z
+inline float axdot(const V3& v, int i) {
+    const float a[3] = {i == 0 ? 1.f : 0.f, i == 1 ? 1.f : 0.f, i == 2 ? 1.f : 0.f};
+    return (v.x * a[0] + v.y * a[1]) + v.z * a[2];
+}
+
+// BoundingVolume of every node (Chunk::Chunk bvh.cpp:81-113, BuildBVs bvh.cpp:235-250) and the
+// node / chunk / triangle tables of the device-side replay.
+void export_octree(const nart_scene_blob& blob, const Octree& o, const std::vector<std::vector<uint32_t>>& chunks,
+                   int root, RefOctree& out) {
+    const float inf = std::numeric_limits<float>::infinity();
+    std::vector<V3> cbmin(chunks.size(), V3{inf, inf, inf}), cbmax(chunks.size(), V3{-inf, -inf, -inf});
+    for (size_t c = 0; c < chunks.size(); ++c)
+        for (uint32_t g : chunks[c]) {
+            const nart_triangle& T = blob.triangles[g];
+            V3 vs[3] = {v3(T.v0), v3(T.v1), v3(T.v2)};
+            float* lo = &cbmin[c].x;
+            float* hi = &cbmax[c].x;
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) {
+                    const float d = axdot(vs[j], i);
+                    lo[i] = gmin(d, lo[i]);
+                    hi[i] = gmax(d, hi[i]);
+                }
+        }
+    const size_t n = o.nodes.size();
+    out.nodes.assign(n, nd::OcNode{});
+    out.chunks.clear();
+    out.tris.clear();
+    out.tri_leaf.assign(blob.num_triangles, -1);
+    out.root = root;
+    for (size_t i = 0; i < n; ++i) {
+        nd::OcNode& d = out.nodes[i];
+        for (int k = 0; k < 3; ++k) {
+            d.bmin[k] = inf;
+            d.bmax[k] = -inf;
+        }
+        d.parent = -1;
+        d.is_leaf = o.nodes[i].isLeaf ? 1 : 0;
+        for (int c = 0; c < 8; ++c) d.children[c] = o.nodes[i].children[c];
+    }
+    for (size_t i = 0; i < n; ++i)
+        for (int c = 0; c < 8; ++c)
+            if (o.nodes[i].children[c] >= 0) out.nodes[o.nodes[i].children[c]].parent = (int32_t)i;
+    // bottom-up extension in BuildBVs' order: leaves over their chunks, inner nodes over children 0..7
+    struct Rec {
+        static void go(const Octree& o, const std::vector<V3>& cbmin, const std::vector<V3>& cbmax,
+                       std::vector<nd::OcNode>& nodes, int i) {
+            nd::OcNode& d = nodes[i];
+            auto ext = [&](const float* lo, const float* hi) {
+                for (int k = 0; k < 3; ++k) {
+                    d.bmin[k] = gmin(d.bmin[k], lo[k]);
+                    d.bmax[k] = gmax(d.bmax[k], hi[k]);
+                }
+            };
+            if (o.nodes[i].isLeaf) {
+                for (int c : o.nodes[i].chunks) ext(&cbmin[c].x, &cbmax[c].x);
+            } else {
+                for (int c = 0; c < 8; ++c) {
+                    const int ch = o.nodes[i].children[c];
+                    if (ch < 0) continue;
+                    go(o, cbmin, cbmax, nodes, ch);
+                    ext(nodes[ch].bmin, nodes[ch].bmax);
+                }
+            }
+        }
+    };
+    Rec::go(o, cbmin, cbmax, out.nodes, root);
+    for (size_t i = 0; i < n; ++i) {
+        nd::OcNode& d = out.nodes[i];
+        d.chunk_first = (uint32_t)(out.chunks.size() / 2);
+        d.chunk_count = 0;
+        if (!o.nodes[i].isLeaf) continue;  // chunks left in a split node are orphaned (bvh.cpp:187-190)
+        for (int c : o.nodes[i].chunks) {
+            out.chunks.push_back((uint32_t)out.tris.size());
+            out.chunks.push_back((uint32_t)chunks[c].size());
+            for (uint32_t g : chunks[c]) {
+                out.tris.push_back(g);
+                out.tri_leaf[g] = (int32_t)i;
+            }
+            ++d.chunk_count;
+        }
+    }
+}
+
 }  // namespace
 
 uint32_t reference_visibility(const nart_scene_blob& blob, std::vector<uint8_t>& mask, bool& root_is_leaf,
-                              uint32_t& n_chunks) {
+                              uint32_t& n_chunks, RefOctree* octree) {
     const float inf = std::numeric_limits<float>::infinity();
     uint32_t numTriangles = 0;
     V3 sMax = {-inf, -inf, -inf}, sMin = {inf, inf, inf};
@@ -141,6 +226,7 @@ uint32_t reference_visibility(const nart_scene_blob& blob, std::vector<uint8_t>&
     }
     mask.assign(blob.num_triangles, 0);
     root_is_leaf = o.nodes[root].isLeaf;
+    if (octree) export_octree(blob, o, chunks, root, *octree);
     if (root_is_leaf) return 0;
     uint32_t vis = 0;
     for (const ONode& n : o.nodes)
@@ -353,7 +439,35 @@ void build_bvh(const nart_scene_blob& blob, const std::vector<uint8_t>& mask, fl
         r[12] = T.v2[2];
         std::memcpy(&r[13], &g, 4);
         r[14] = 0.f;
-        r[15] = 0.f;
+        r[15] = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]) * 0.125f;  // |n| cos(82.8 deg), octree.h
+    }
+}
+
+// tri_isect word 14: the triangle's reference-octree leaf (bits 0-30) and bit 31 set when the
+// whole triangle lies inside that leaf's box by `margin` on every axis (no flat axis).  A hit on
+// it whose ray is not grazing (|dot(d, n)| >= |n| / 8, word 15; the plane distance t then places
+// o + t d within ~250 ulps of the scene scale of the triangle) is clear of the leaf's faces,
+// and octree.h needs no box loads for it.
+void annotate_octree_leaves(const nart_scene_blob& blob, const RefOctree& oct, float margin, BuiltBVH& bvh) {
+    const size_t n = bvh.tri_isect.size() / 16;
+    for (size_t i = 0; i < n; ++i) {
+        float* r = &bvh.tri_isect[i * 16];
+        uint32_t g;
+        std::memcpy(&g, &r[13], 4);
+        const int32_t leaf = g < oct.tri_leaf.size() ? oct.tri_leaf[g] : -1;
+        uint32_t info = leaf >= 0 ? (uint32_t)leaf : 0u;
+        if (leaf >= 0) {
+            const nd::OcNode& L = oct.nodes[leaf];
+            const nart_triangle& T = blob.triangles[g];
+            bool inside = true;
+            for (int k = 0; k < 3 && inside; ++k) {
+                const float lo = std::min(T.v0[k], std::min(T.v1[k], T.v2[k]));
+                const float hi = std::max(T.v0[k], std::max(T.v1[k], T.v2[k]));
+                inside = L.bmin[k] < L.bmax[k] && lo - L.bmin[k] >= margin && L.bmax[k] - hi >= margin;
+            }
+            if (inside) info |= 0x80000000u;
+        }
+        std::memcpy(&r[14], &info, 4);
     }
 }
 

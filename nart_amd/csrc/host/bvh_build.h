@@ -19,15 +19,28 @@ struct BuiltBVH {
     float pad = 0.f;                   // box padding applied (world units)
 };
 
+// The reference octree itself, for exact emulation of Octree::Intersect on the device.
+struct RefOctree {
+    std::vector<nd::OcNode> nodes;  // creation order, root first
+    std::vector<uint32_t> chunks;   // (tri_first, tri_count) per leaf chunk, leaves in node order
+    std::vector<uint32_t> tris;     // global triangle ids
+    std::vector<int32_t> tri_leaf;  // per scene triangle: its leaf, -1 if unreachable
+    int32_t root = 0;
+};
+
 // Which triangles the reference's octree can ever return (bvh.cpp:252-326): all of them
 // unless the root stayed a leaf (single chunk, bvh.cpp:131 -> nothing is hit) or a leaf
 // holding several chunks split and dropped all but one (bvh.cpp:187-190).
 // Returns the number of visible triangles; mask[g] = 1 for visible ones.
 uint32_t reference_visibility(const nart_scene_blob& blob, std::vector<uint8_t>& mask, bool& root_is_leaf,
-                              uint32_t& n_chunks);
+                              uint32_t& n_chunks, RefOctree* octree = nullptr);
 
 // Binned-SAH BVH2 over the visible triangles.  Child boxes are padded by `pad` (world units)
 // so the device's fast slab test is conservative w.r.t. the exact triangle test.
 void build_bvh(const nart_scene_blob& blob, const std::vector<uint8_t>& mask, float pad, BuiltBVH& out);
+
+// Tag each BVH triangle with its octree leaf and whether it lies inside the leaf's box by
+// `margin` (device/octree.h fast path).
+void annotate_octree_leaves(const nart_scene_blob& blob, const RefOctree& oct, float margin, BuiltBVH& bvh);
 
 }  // namespace nart

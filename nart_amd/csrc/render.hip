@@ -38,6 +38,12 @@ struct nart_ctx {
     void* d_tex_pool = nullptr;
     void* d_envs = nullptr;
     void* d_density = nullptr;
+    void* d_oc_nodes = nullptr;   // reference octree (octree.h)
+    void* d_oc_chunks = nullptr;
+    void* d_oc_tris = nullptr;
+    void* d_tri_leaf = nullptr;
+    void* d_oc_lock = nullptr;    // replay heap pool
+    void* d_oc_heap = nullptr;
     std::vector<void*> env_bufs;  // Piecewise2DDistribution tables
     // work buffers
     size_t cap_slot_bytes = 0, cap_misc = 0;
@@ -586,6 +592,8 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
             stats->node_visits += c[2];
             stats->tri_tests += c[3];
             stats->bounces += c[4];
+            stats->octree_checks += c[5];
+            stats->octree_replays += c[6];
         }
     }
     return NART_OK;
@@ -621,7 +629,8 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     std::vector<uint8_t> mask;
     bool root_leaf = false;
     uint32_t n_chunks = 0;
-    nart::reference_visibility(*blob, mask, root_leaf, n_chunks);
+    nart::RefOctree oct;
+    nart::reference_visibility(*blob, mask, root_leaf, n_chunks, &oct);
     float maxabs = 1.f;
     for (uint32_t g = 0; g < blob->num_triangles; ++g) {
         const nart_triangle& T = blob->triangles[g];
@@ -632,6 +641,9 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     for (int k = 3; k < 16; k += 4) maxabs = std::max(maxabs, std::fabs(blob->camera.m[k]));
     nart::BuiltBVH bvh;
     nart::build_bvh(*blob, mask, maxabs * 6.103515625e-05f + 1e-6f, bvh);
+    // hit points deviate from the reference's slab arithmetic by far less than 2^-14 * scene
+    // scale (|o| + |t d| <= 3 * maxabs, errors of a few ulps): octree.h oc_clear
+    nart::annotate_octree_leaves(*blob, oct, maxabs * 6.103515625e-05f, bvh);
     ctx->stack_depth = std::max<uint32_t>(bvh.max_stack + 1, 2);
     if ((rc = upload(ctx, ctx->d_nodes, bvh.nodes.data(), bvh.nodes.size()))) return bail(rc);
     ctx->num_nodes = (uint32_t)bvh.nodes.size();
@@ -710,6 +722,28 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     std::memcpy(S.cam_m, blob->camera.m, sizeof(S.cam_m));
     // glm::tan(glm::radians(fov)) with the host libm, as the reference (pinholecamera.cpp:20)
     S.cam_tan = std::tan(blob->camera.fov * (float)0.01745329251994329576923690768489);
+    // reference octree + replay heap pool: one slot per 32 resident lanes (a slot is held only
+    // while a lane replays), at least 4096 and within 256 MiB
+    if ((rc = upload(ctx, ctx->d_oc_nodes, oct.nodes.data(), oct.nodes.size()))) return bail(rc);
+    if ((rc = upload(ctx, ctx->d_oc_chunks, oct.chunks.data(), oct.chunks.size()))) return bail(rc);
+    if ((rc = upload(ctx, ctx->d_oc_tris, oct.tris.data(), oct.tris.size()))) return bail(rc);
+    if ((rc = upload(ctx, ctx->d_tri_leaf, oct.tri_leaf.data(), oct.tri_leaf.size()))) return bail(rc);
+    S.oc_nodes = (const OcNode*)ctx->d_oc_nodes;
+    S.oc_chunks = (const uint32_t*)ctx->d_oc_chunks;
+    S.oc_tris = (const uint32_t*)ctx->d_oc_tris;
+    S.tri_leaf = (const int32_t*)ctx->d_tri_leaf;
+    S.oc_root = oct.root;
+    S.oc_cap = (uint32_t)std::max<size_t>(oct.nodes.size(), 1);
+    S.oc_pool = (uint32_t)std::max<size_t>(64, std::min<size_t>(4096, (256ull << 20) / (8ull * S.oc_cap)));
+    S.oc_scale = maxabs;
+    S.oc_exact = 1;
+    if (const char* v = std::getenv("NART_OCTREE_EXACT")) S.oc_exact = std::atoi(v) != 0;
+    if (hipMalloc(&ctx->d_oc_lock, sizeof(uint32_t) * S.oc_pool) != hipSuccess ||
+        hipMemset(ctx->d_oc_lock, 0, sizeof(uint32_t) * S.oc_pool) != hipSuccess ||
+        hipMalloc(&ctx->d_oc_heap, sizeof(unsigned long long) * S.oc_pool * S.oc_cap) != hipSuccess)
+        return bail(NART_E_OOM);
+    S.oc_lock = (uint32_t*)ctx->d_oc_lock;
+    S.oc_heap = (unsigned long long*)ctx->d_oc_heap;
     *out = ctx;
     return NART_OK;
 }
@@ -719,7 +753,8 @@ void nart_hip_destroy(nart_ctx* ctx) {
     hipSetDevice(ctx->device);
     void* bufs[] = {ctx->d_nodes, ctx->d_tri_isect, ctx->d_tris, ctx->d_tri_mesh, ctx->d_meshes, ctx->d_mats,
                     ctx->d_lights, ctx->d_texs, ctx->d_tex_pool, ctx->d_slot_xy, ctx->d_rng, ctx->d_samples,
-                    ctx->d_L, ctx->d_bucket_ids, ctx->d_bucket_base, ctx->d_table, ctx->d_counters, ctx->d_wf, ctx->d_envs, ctx->d_density};
+                    ctx->d_L, ctx->d_bucket_ids, ctx->d_bucket_base, ctx->d_table, ctx->d_counters, ctx->d_wf, ctx->d_envs, ctx->d_density,
+                    ctx->d_oc_nodes, ctx->d_oc_chunks, ctx->d_oc_tris, ctx->d_tri_leaf, ctx->d_oc_lock, ctx->d_oc_heap};
     for (void* b : bufs)
         if (b) hipFree(b);
     for (void* b : ctx->env_bufs) hipFree(b);

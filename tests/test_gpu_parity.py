@@ -215,3 +215,37 @@ def test_bucket_api_matches_render(gpu, glass_gpu, glass_scene):
     torch.cuda.synchronize()
     ref = glass_gpu.render(p)
     assert _bits_equal(img.cpu().numpy(), ref)
+
+
+# C2 buckets (1920x1080x64) where the reference octree's unpadded slab tests reject the box
+# holding the true closest hit (or a shadow blocker): found by tools/full_parity.py c2 before
+# device/octree.h reproduced Octree::Intersect's reachability.
+C2_OCTREE_BUCKETS = [1356, 1403, 1476, 1700, 1820, 2676, 3203, 4020, 4121, 5083, 5196, 6922, 7286, 7820, 8106]
+
+
+@pytest.mark.parametrize("variant", VARIANTS, ids=["megakernel", "wavefront"])
+def test_octree_boundary_rejections(gpu, cornell_scene, variant):
+    import torch
+    p = _params(cornell_scene, 1920, 1080, 64)
+    g = nart_amd.session_geometry(p)
+    ids = np.array(C2_OCTREE_BUCKETS, np.uint32)
+    tiles = torch.zeros((len(ids), g.tile_size * g.tile_size, 5), dtype=torch.float32, device="cuda")
+    gpu_r = nart_amd.HipRenderer(cornell_scene, variant=variant)
+    st = nart_amd.RenderStats()
+    gpu_r.set_counters(True)
+    gpu_r.render_buckets_async(p, ids, tiles.data_ptr(), torch.cuda.current_stream().cuda_stream, st)
+    torch.cuda.synchronize()
+    ref = oracle.Oracle(cornell_scene).render_buckets(p, ids)
+    got = tiles.cpu().numpy()
+    assert _bits_equal(got, ref), _report(got, ref)
+    assert st.octree_replays > 0  # the emulation, not luck, decided these buckets
+
+
+def test_octree_missed_camera_hit_samples(gpu, cornell_scene):
+    """C2 pixel (331, 235): the octree misses triangle 465 at t = 3.1 for sample 30's camera ray
+    and the reference renders that sample as a miss (alpha 0)."""
+    p = _params(cornell_scene, 1920, 1080, 64)
+    gs = nart_amd.HipRenderer(cornell_scene).render_samples(p, 328, 232, 8, 8)
+    rs = oracle.Oracle(cornell_scene).render_samples(p, 328, 232, 8, 8)
+    assert rs[3, 3, 30, 3] == 0.0
+    assert _bits_equal(gs, rs), _report(gs, rs)
