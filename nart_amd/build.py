@@ -68,7 +68,8 @@ def build_hip_lib(force=False):
     srcs = _sources("render.hip", "device", "host") + [os.path.join(REPO, "include", "nart_hip.h"), scene]
     if not force and _newer(out, srcs):
         return out
-    _run([hipcc(), "--offload-arch=" + ARCH, "-fhip-fp32-correctly-rounded-divide-sqrt"] + COMMON +
+    extra = os.environ.get("NART_HIP_DEFINES", "").split()  # development builds, e.g. -DNART_WAVEPROF
+    _run([hipcc(), "--offload-arch=" + ARCH, "-fhip-fp32-correctly-rounded-divide-sqrt"] + COMMON + extra +
          ["-shared", "-o", out, os.path.join(CSRC, "render.hip"), os.path.join(CSRC, "host", "bvh_build.cpp"),
           "-L" + LIB, "-lnart_scene", "-Wl,-rpath,$ORIGIN"])
     return out

@@ -85,6 +85,13 @@ struct RenderArgs {
     float gamma;              // roughening factor squared (pathintegrator.cpp:163)
     unsigned long long* counters;  // [5] extend rays, shadow rays, node visits, tri tests, bounces
     uint32_t lds_nodes;       // BVH nodes [0, lds_nodes) staged in LDS after the stack
+    // Pixel work queue (k_render): lane g starts on slot queue[g]; with qhead set the grid is
+    // persistent and a lane whose pixel is done takes queue[qbase + atomicAdd(qhead)].
+    const uint32_t* queue = nullptr;
+    uint32_t* qhead = nullptr;
+    uint32_t qbase = 0;
+    uint32_t* cost = nullptr; // cost probe: per-slot work estimate of the rendered sample(s)
+    uint32_t sstride = 0;     // per-slot stride of samples / Lout (= spp except in the cost probe)
 };
 
 // Stage the top BVH nodes (breadth-first prefix) into LDS; every thread of the block calls it.
@@ -168,6 +175,14 @@ enum { ST_EXT = 0, ST_SH1 = 1, ST_SH2 = 2 };
 #ifndef NART_RENDER_WAVES
 #define NART_RENDER_WAVES 2
 #endif
+// development profile: cycles per code section of the path kernel, printed for slot 0
+#ifdef NART_SECTPROF
+#define SECT_T() __builtin_amdgcn_s_memtime()
+#define SECT(i, t) (sect[i] += SECT_T() - (t))
+#else
+#define SECT_T() 0ull
+#define SECT(i, t) ((void)0)
+#endif
 #define NART_RENDER_LB __launch_bounds__(256, NART_RENDER_WAVES)
 template <int MAXL, bool COUNT, bool ENV>
 __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
@@ -180,13 +195,26 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
     stage_nodes(S, s_nodes, A.lds_nodes);
     const int nl = (int)A.lds_nodes;
     const int tid = threadIdx.x;
-    const uint32_t slot = blockIdx.x * blockDim.x + tid;
-    if (slot >= A.n_slots) return;
-    const uint32_t xy = A.slot_xy[slot];
-    const uint32_t px = xy & 0xFFFFu, py = xy >> 16;
-    uint32_t rng = A.rng0[slot];
-    const float2* smp = A.samples + (size_t)slot * A.spp;
-    float4* out = A.Lout + (size_t)slot * A.spp;
+    const uint32_t gid = blockIdx.x * blockDim.x + tid;
+    uint32_t slot = gid;
+    if (A.queue) {
+        slot = gid < A.n_slots ? A.queue[gid] : 0xFFFFFFFFu;
+    } else if (slot >= A.n_slots) {
+        return;
+    }
+    uint32_t px = 0, py = 0, rng = 0;
+    const float2* smp = A.samples;
+    float4* out = A.Lout;
+    auto take_pixel = [&](uint32_t sl) {
+        slot = sl;
+        const uint32_t xy = A.slot_xy[sl];
+        px = xy & 0xFFFFu;
+        py = xy >> 16;
+        rng = A.rng0[sl];
+        smp = A.samples + (size_t)sl * A.sstride;
+        out = A.Lout + (size_t)sl * A.sstride;
+    };
+    if (slot != 0xFFFFFFFFu) take_pixel(slot);
     int* sc = s_code + tid;
     float* stn = s_tn + tid;
     const int stride = blockDim.x;
@@ -194,7 +222,8 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
     TraceCounters cnt = {0u, 0u, 0u, 0u};
     uint32_t n_ext = 0, n_sh = 0, n_bounce = 0;
 
-    uint32_t s = 0;
+    uint32_t s = slot != 0xFFFFFFFFu ? 0u : A.spp;
+    uint32_t iters = 0;  // outer iterations of this lane (cost probe)
     f3 L, beta, Le, c1, c2, betak, Led;
     float alpha = 0.f, eta_sampled = 1.f, eta_outer = 1.f, alphaTweak = 1.f;
     uint32_t flags = 0, bounce = 0;
@@ -206,7 +235,38 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
     bool lightHit = false, use1 = false, use2 = false, cont = false, have_ed = false;
     bool new_sample = true, new_bounce = false;
 
+#ifdef NART_WAVEPROF
+    const uint64_t prof_t0 = __builtin_amdgcn_s_memtime();
+    const bool prof_lead = tid % 64 == 0;
+    uint32_t prof_maxcall = 0;
+    uint64_t prof_iters = 0, prof_trav = 0;
+#endif
+#ifdef NART_SECTPROF
+    uint64_t sect[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint64_t sect_t0 = SECT_T();
+#endif
     for (;;) {
+        uint64_t st0 = SECT_T();
+        if (A.qhead) {
+            // refill lanes whose pixel is done: one queue atomic per wave
+            const bool need = new_sample && s >= A.spp;
+            const uint64_t m = __ballot(need);
+            if (m) {
+                const int leader = __builtin_ctzll(m);
+                uint32_t base = 0;
+                if ((int)__lane_id() == leader) base = atomicAdd(A.qhead, (uint32_t)__popcll(m));
+                base = __builtin_amdgcn_readlane(base, leader);
+                if (need) {
+                    const uint32_t idx = A.qbase + base +
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    if (idx < A.n_slots) {
+                        take_pixel(A.queue[idx]);
+                        s = 0;
+                    }
+                }
+            }
+        }
+        ++iters;
         if (new_sample) {
             if (s >= A.spp) break;
             float2 sm = smp[s];
@@ -223,6 +283,8 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
             new_sample = false;
             new_bounce = true;
         }
+        SECT(0, st0);
+        st0 = SECT_T();
         if (new_bounce) {
             new_bounce = false;
             if (bounce >= A.bounces) {
@@ -250,11 +312,35 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
             stage = ST_EXT;
             if (COUNT) ++n_ext;
         }
+        SECT(1, st0);
+        st0 = SECT_T();
 
         float bt;
         uint32_t bg;
+#ifdef NART_WAVEPROF
+        const uint64_t prof_t1 = __builtin_amdgcn_s_memtime();
+        const uint32_t prof_n0 = cnt.nodes, prof_t0n = cnt.tris;
+        ++prof_iters;
+#endif
         const bool hit = traverse<COUNT>(S, cur, tmax, stage != ST_EXT, bt, bg, sc, stn, stride, cnt, s_nodes, nl);
+#ifdef NART_WAVEPROF
+        if (COUNT) {
+            const uint32_t dn = cnt.nodes - prof_n0;
+            prof_maxcall = dn > prof_maxcall ? dn : prof_maxcall;
+            if (dn > 1500 && atomicAdd(&A.counters[20], 1ull) < 12)
+                printf("WAVEPROF long query nodes %u tris %u stage %d px (%u,%u) s %u bounce %u o %a %a %a d %a %a %a tmax %a hit %d\n",
+                       dn, cnt.tris - prof_t0n, stage, px, py, s, bounce, cur.o.x, cur.o.y, cur.o.z, cur.d.x, cur.d.y, cur.d.z,
+                       tmax, (int)hit);
+            const uint64_t _e = __ballot(1);
+            const uint64_t dtr = __builtin_amdgcn_s_memtime() - prof_t1;
+            prof_trav += dtr;
+            if ((int)__lane_id() == __builtin_ctzll(_e)) cnt.pw[6] += dtr;
+            if (stage == ST_EXT && hit) WPROF(cnt, 8);
+        }
+#endif
 
+        SECT(2, st0);
+        st0 = SECT_T();
         bool resolve = false;
         if (stage == ST_EXT) {
             if (!hit) {
@@ -275,6 +361,8 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
             if (list.valid(is.meshID, is.priority, eta_outer)) {
                 if (bounce == 0) alpha = 1.f;
                 const f3 wo = to_local(bsdf, neg(cur.d));
+                SECT(3, st0);
+                st0 = SECT_T();
                 // ---- EstimateDirect (pathintegrator.cpp:38-121)
                 const DLight& Lg = S.lights[f2u8(gmin(rng_float(rng), ND_ONE_MINUS_EPS) * nL)];
                 float sPdf = 0.f, lPdf = 0.f;
@@ -305,6 +393,8 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
                         }
                     }
                 }
+                SECT(4, st0);
+                st0 = SECT_T();
                 lPdf = 0.f;
                 float lx = rng_float(rng);
                 float ly = rng_float(rng);
@@ -328,6 +418,8 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
                 }
                 betak = beta;
                 have_ed = true;
+                SECT(5, st0);
+                st0 = SECT_T();
                 // ---- continuation (pathintegrator.cpp:199-220)
                 float a = rng_float(rng);
                 float b = rng_float(rng);
@@ -364,6 +456,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
                 }
             }
             ++bounce;
+            SECT(6, st0);
             Led = F3(0.f, 0.f, 0.f);
             if (use1) {
                 stage = ST_SH1;
@@ -403,6 +496,37 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
                 new_sample = true;
             }
         }
+    }
+#ifdef NART_SECTPROF
+    sect[7] = SECT_T() - sect_t0;
+    if (slot == 0)
+        printf("SECTPROF new_sample %llu new_bounce %llu traverse %llu isect_bsdf %llu ed_bsdf %llu ed_light %llu cont %llu total %llu\n",
+               (unsigned long long)sect[0], (unsigned long long)sect[1], (unsigned long long)sect[2], (unsigned long long)sect[3],
+               (unsigned long long)sect[4], (unsigned long long)sect[5], (unsigned long long)sect[6], (unsigned long long)sect[7]);
+#endif
+#ifdef NART_WAVEPROF
+    if (COUNT) {
+        if (prof_lead) {
+            const uint64_t dt = __builtin_amdgcn_s_memtime() - prof_t0;
+            cnt.pw[7] += dt;
+            unsigned long long* wv = A.counters + 24 + 8 * (size_t)(gid / 64);
+            wv[0] = dt;
+            wv[3] = slot;
+        }
+        unsigned long long* wv = A.counters + 24 + 8 * (size_t)(gid / 64);
+        if (!A.queue) A.counters[24 + 8 * 70000 + slot] = ((unsigned long long)(n_ext + n_sh) << 32) | cnt.nodes;  // per-slot cost
+        atomicMax(&wv[1], (unsigned long long)prof_trav);  // traversal cycles of the longest lane
+        atomicMax(&wv[2], (unsigned long long)prof_iters); // outer loop iterations of the longest lane
+        atomicAdd(&wv[4], (unsigned long long)cnt.pw[2]);
+        atomicAdd(&wv[5], (unsigned long long)cnt.nodes);
+        atomicAdd(&wv[6], (unsigned long long)cnt.pw[4]);
+        atomicAdd(&wv[7], (unsigned long long)cnt.tris);
+        for (int i = 0; i < 10; ++i) atomicAdd(&A.counters[8 + i], (unsigned long long)cnt.pw[i]);
+    }
+#endif
+    if (A.cost) {  // cost probe (one pixel per lane, no queue): node/triangle/iteration weights
+        A.cost[gid] = cnt.nodes + 2u * cnt.tris + 30u * iters;
+        return;
     }
     if (COUNT) {
         atomicAdd(&A.counters[0], (unsigned long long)n_ext);

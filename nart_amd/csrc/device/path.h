@@ -72,7 +72,26 @@ ND bool edges_accept(float e0, float e1, float e2) {  // geometry.cpp:78-81
 struct TraceCounters {
     uint32_t nodes, tris;
     uint32_t oc_checks, oc_replays;  // octree.h: exact ancestor checks, octree replays
+#ifdef NART_WAVEPROF
+    // development profile (counter pass only): wave-level iterations and active lanes of the
+    // traversal step / node / triangle loops, cycles in traversal and in total
+    uint64_t pw[10];
+#endif
 };
+#ifdef NART_WAVEPROF
+#define WPROF(cnt, i)                                                  \
+    do {                                                               \
+        const uint64_t _e = __ballot(1);                               \
+        if ((int)__lane_id() == __builtin_ctzll(_e)) {                 \
+            (cnt).pw[i]++;                                             \
+            (cnt).pw[(i) + 1] += (uint64_t)__popcll(_e);               \
+        }                                                              \
+    } while (0)
+#else
+#define WPROF(cnt, i) \
+    do {              \
+    } while (0)
+#endif
 
 // Closest hit (ANY=false): minimum (t, scene index) over triangles with 0 < t < tmax whose
 // sheared edge test passes -- the set Octree::Intersect selects from (bvh.cpp:132-176).
@@ -144,14 +163,27 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
                   const float4* lnodes, int nl) {
     while (t.code >= 0) {
         if (COUNT) cnt.nodes++;
+        if (COUNT) WPROF(cnt, 2);
         float4 a, b, c;
         int4 k;
         if (t.code < nl) {
+#if !defined(NART_NODE_FLAT) && defined(__HIP_DEVICE_COMPILE__)
+            // explicit LDS address space: ds_read_b128, not a flat load through the generic aperture
+            typedef float v4f __attribute__((ext_vector_type(4)));
+            typedef const __attribute__((address_space(3))) v4f lds_v4f;
+            lds_v4f* np = (lds_v4f*)lnodes + 4 * t.code;
+            const v4f qa = np[0], qb = np[1], qc = np[2], qk = np[3];
+            a = make_float4(qa.x, qa.y, qa.z, qa.w);
+            b = make_float4(qb.x, qb.y, qb.z, qb.w);
+            c = make_float4(qc.x, qc.y, qc.z, qc.w);
+            k = make_int4(__float_as_int(qk.x), __float_as_int(qk.y), __float_as_int(qk.z), __float_as_int(qk.w));
+#else
             const float4* np = lnodes + 4 * t.code;
             a = np[0];
             b = np[1];
             c = np[2];
             k = reinterpret_cast<const int4*>(np)[3];
+#endif
         } else {
             const float4* np = reinterpret_cast<const float4*>(S.nodes + t.code);
             a = np[0];
@@ -189,14 +221,34 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
     }
     const uint32_t lc = ~(uint32_t)t.code;
     const uint32_t first = lc >> 5, count = (lc & 31u) + 1u;
+#ifndef NART_TRI_SERIAL
+    // software-pipelined leaf: the records of triangle i + 1 are in flight while triangle i is
+    // tested (the last iteration reloads its own record instead of reading past the leaf)
+    const float4* tp0 = S.tri_isect + 4 * first;
+    float4 na = tp0[0], nb = tp0[1], nc = tp0[2], nd = tp0[3];
+#endif
     for (uint32_t i = 0; i < count; ++i) {
         if (COUNT) cnt.tris++;
+        if (COUNT) WPROF(cnt, 4);
+#ifndef NART_TRI_SERIAL
+        const float4 a = na, b = nb, c = nc, dd = nd;
+        {
+            const float4* tq = tp0 + 4 * (i + 1 < count ? i + 1 : i);
+            na = tq[0];
+            nb = tq[1];
+            nc = tq[2];
+            nd = tq[3];
+        }
+#else
         const float4* tp = S.tri_isect + 4 * (first + i);
         float4 b = tp[1], c = tp[2], dd = tp[3];
+#endif
         float e0, e1, e2;
         edge_functions(r, F3(b.x, b.y, b.z), F3(b.w, c.x, c.y), F3(c.z, c.w, dd.x), e0, e1, e2);
         if (!edges_accept(e0, e1, e2)) continue;
+#ifdef NART_TRI_SERIAL
         float4 a = tp[0];
+#endif
         f3 n = F3(a.x, a.y, a.z);
         const float den = dot(r.d, n);
         float tt = (a.w - dot(r.o, n)) / den;
@@ -240,7 +292,9 @@ ND bool traverse(const DScene& S, const Ray& r, float tmax, bool ANY, float& bes
     if (!S.geometry_visible) return false;
     Trav t;
     trav_begin(S, r, tmax, ANY, t);
+    if (COUNT) WPROF(cnt, 0);
     while (!trav_step<COUNT>(S, r, t, sc, st, stride, cnt, lnodes, nl)) {
+        if (COUNT) WPROF(cnt, 0);
     }
     bestT = t.bestT;
     bestG = t.bestG;

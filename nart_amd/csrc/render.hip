@@ -1,9 +1,12 @@
 // C-ABI of the MI355X render path (include/nart_hip.h): context creation (scene upload, BVH
 // build, light precomputation) and the Render()-equivalent launch sequence.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -66,6 +69,15 @@ struct nart_ctx {
     uint32_t wf_grid_trace = 0, wf_grid_shade = 0;
     uint64_t wf_iterations = 0;
     uint64_t stat_counts[5] = {0, 0, 0, 0, 0};
+    // megakernel work queue (launch_render)
+    uint32_t* d_queue = nullptr;
+    uint32_t* d_cost = nullptr;
+    uint32_t* d_keys[2] = {nullptr, nullptr};
+    uint32_t* d_vals[2] = {nullptr, nullptr};
+    uint32_t* d_qhead = nullptr;
+    void* d_sort_tmp = nullptr;
+    size_t cap_sort_tmp = 0;
+    uint32_t cap_queue = 0;
 };
 
 namespace {
@@ -289,6 +301,32 @@ int ensure(nart_ctx* ctx, size_t slots, uint32_t spp, size_t buckets) {
     return NART_OK;
 }
 
+// Work-queue buffers of the megakernel scheduler (queue, cost probe, radix-sort scratch).
+int ensure_queue(nart_ctx* ctx, uint32_t n) {
+    if (n <= ctx->cap_queue) return NART_OK;
+    void** bufs[7] = {(void**)&ctx->d_queue, (void**)&ctx->d_cost, (void**)&ctx->d_keys[0], (void**)&ctx->d_keys[1],
+                      (void**)&ctx->d_vals[0], (void**)&ctx->d_vals[1], (void**)&ctx->d_qhead};
+    for (void** b : bufs) {
+        if (*b) hipFree(*b);
+        *b = nullptr;
+    }
+    if (ctx->d_sort_tmp) hipFree(ctx->d_sort_tmp);
+    ctx->d_sort_tmp = nullptr;
+    ctx->cap_queue = 0;
+    for (int i = 0; i < 6; ++i) HIPCHK(hipMalloc(bufs[i], (size_t)n * 4));
+    HIPCHK(hipMalloc(bufs[6], 256));
+    size_t tmp = 0, t1 = 0, t2 = 0;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, ctx->d_keys[0], ctx->d_keys[1], ctx->d_vals[0],
+                                              ctx->d_vals[1], (int)n, 0, 1));
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, t2, ctx->d_keys[0], ctx->d_keys[1], ctx->d_vals[0],
+                                              ctx->d_vals[1], (int)((n + 63) / 64), 0, 32));
+    tmp = std::max(t1, t2);
+    HIPCHK(hipMalloc(&ctx->d_sort_tmp, tmp + 256));
+    ctx->cap_sort_tmp = tmp + 256;
+    ctx->cap_queue = n;
+    return NART_OK;
+}
+
 // LDS of one k_render block: traversal stack + as many top BVH nodes as fit while
 // NART_RENDER_WAVES blocks share a CU's 160 KiB (NART_LDS_NODES overrides the node count).
 uint32_t render_lds_nodes(const nart_ctx* ctx) {
@@ -299,34 +337,170 @@ uint32_t render_lds_nodes(const nart_ctx* ctx) {
     return (uint32_t)std::min<size_t>(n, ctx->num_nodes);
 }
 
+// ---------------------------------------------------------------- megakernel scheduling
+// A pixel's samples are one serial chain (its RNG stream), so a frame can finish no earlier
+// than its costliest pixels, and a wave of 64 costly pixels runs several times longer than one
+// such pixel alone (the wave executes the union of its lanes' work).  With the work queue the
+// grid is persistent: lanes take pixels from a queue ordered by a cost probe (one sample per
+// pixel), the costliest pixels spread over all waves so that each holds only a few of them,
+// and a lane whose pixel is done takes the next one instead of idling until its wave ends.
+// The image is unchanged (each pixel's samples stay on its own RNG stream).
+//   NART_QUEUE=0  one lane per pixel, no queue (the launch order is the slot order)
+//   NART_QUEUE=1  persistent lanes, queue in slot order
+//   NART_QUEUE=2  persistent lanes, queue ordered by the cost probe (default)
+
+// Group (wave-sized run of 64 consecutive slots: a 16x4 strip of a bucket) costs, as keys of an
+// ascending sort that puts the costliest group first; a partial last group always sorts last.
+__global__ void k_group_keys(const uint32_t* cost, uint32_t n, uint32_t* keys, uint32_t* vals) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t ng = (n + 63) / 64;
+    if (g >= ng) return;
+    uint64_t sum = 0;
+    const uint32_t e = min(n, 64 * g + 64);
+    for (uint32_t i = 64 * g; i < e; ++i) sum += cost[i];
+    const uint32_t c = (uint32_t)min<uint64_t>(sum, 0xFFFFFFFEull);
+    keys[g] = (e - 64 * g < 64) ? 0xFFFFFFFFu : 0xFFFFFFFEu - c;
+    vals[g] = g;
+}
+
+// Pixel list of the sorted groups (group order, slot order inside a group).
+__global__ void k_expand_groups(const uint32_t* groups, uint32_t n, uint32_t* pixels) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    pixels[r] = 64 * groups[r / 64] + r % 64;
+}
+
+// Mark the k*W costliest pixels (ranks [0, E) of the class-sorted list) for the 1-bit partition.
+__global__ void k_flag_top(const uint32_t* sorted, uint32_t n, uint32_t E, uint32_t* flag) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    flag[sorted[r]] = r < E ? 1u : 0u;
+}
+
+// Queue: in the first round of W waves, lanes j < k of wave w take the costly pixel of rank
+// j*W + w (each wave holds k of them); every other position takes the remaining pixels in
+// slot order (spatially coherent waves).
+__global__ void k_build_queue(const uint32_t* top, const uint32_t* rest, uint32_t n, uint32_t W, uint32_t k,
+                              uint32_t* queue) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t g = 64u * W;
+    if (p < g) {
+        const uint32_t w = p / 64u, j = p % 64u;
+        queue[p] = j < k ? top[j * W + w] : rest[w * (64u - k) + (j - k)];
+    } else {
+        queue[p] = rest[(64u - k) * W + (p - g)];
+    }
+}
+
+__global__ void k_iota(uint32_t* v, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = i;
+}
+
+int queue_mode() {
+    static int m = -1;
+    if (m < 0) {
+        const char* e = std::getenv("NART_QUEUE");
+        m = e ? std::max(0, std::min(2, std::atoi(e))) : 2;
+    }
+    return m;
+}
+
 template <int MAXL, bool COUNT, bool ENV>
-void launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
+int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
+    auto kern = k_render<MAXL, COUNT, ENV>;
     static bool attr = false;  // dynamic LDS above the 64 KiB default
     if (!attr) {
-        hipFuncSetAttribute((const void*)k_render<MAXL, COUNT, ENV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_render<MAXL, true, ENV>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             160 * 1024);
         attr = true;
     }
     RenderArgs b = a;
     b.lds_nodes = render_lds_nodes(ctx);
-    dim3 grid((a.n_slots + 255) / 256), block(256);
-    size_t lds = (size_t)ctx->stack_depth * 256 * 8 + (size_t)b.lds_nodes * sizeof(BVHNode);
-    hipLaunchKernelGGL((k_render<MAXL, COUNT, ENV>), grid, block, lds, st, ctx->scene, b);
+    const size_t lds = (size_t)ctx->stack_depth * 256 * 8 + (size_t)b.lds_nodes * sizeof(BVHNode);
+    const dim3 block(256);
+    uint32_t blocks = (a.n_slots + 255) / 256;
+    const int mode = queue_mode();
+    if (mode > 0) {
+        int cus = 0, per_cu = 0;
+        HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 256, lds));
+        const uint32_t resident = (uint32_t)std::max(1, cus * std::max(per_cu, 1));
+        if (blocks > resident) {  // more pixels than resident lanes: persistent grid + queue
+            const uint32_t n = a.n_slots;
+            int rc = ensure_queue(ctx, n);
+            if (rc) return rc;
+            const dim3 eg((n + 255) / 256);
+            const uint32_t W = resident * 4;  // persistent waves
+            // costly pixels per first-round wave: few when the shard is small (their serial chains
+            // bound the frame), all 64 (packed, launched first) when there are many rounds
+            const double R = (double)n / (64.0 * W);
+            uint32_t k = R >= 3.0 ? 32u : 8u;  // measured on C3 shards of 1/2, 1/4, 1/8 of the frame
+            if (R >= 12.0 && mode == 2 && !std::getenv("NART_QUEUE_K")) {
+                // many rounds: the slot order (costly waves interleaved with cheap ones in time)
+                // measured faster than any reordering; no probe
+                hipLaunchKernelGGL(kern, dim3(blocks), block, lds, st, ctx->scene, b);
+                HIPCHK(hipGetLastError());
+                return NART_OK;
+            }
+            if (const char* e = std::getenv("NART_QUEUE_K")) k = (uint32_t)std::max(1, std::min(64, std::atoi(e)));
+            const bool refill = k < 64u || mode == 1;
+            if (mode == 1) {
+                hipLaunchKernelGGL(k_iota, eg, block, 0, st, ctx->d_queue, n);
+            } else {
+                RenderArgs pb = b;  // cost probe: the first sample of every pixel
+                pb.spp = 1;
+                pb.cost = ctx->d_cost;
+                hipLaunchKernelGGL((k_render<MAXL, true, ENV>), dim3(blocks), block, lds, st, ctx->scene, pb);
+                const uint32_t ng = (n + 63) / 64;
+                hipLaunchKernelGGL(k_group_keys, dim3((ng + 255) / 256), block, 0, st, ctx->d_cost, n, ctx->d_keys[0],
+                                   ctx->d_vals[0]);
+                size_t tmp = ctx->cap_sort_tmp;
+                HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->d_sort_tmp, tmp, ctx->d_keys[0], ctx->d_keys[1],
+                                                          ctx->d_vals[0], ctx->d_vals[1], (int)ng, 0, 32, st));
+                hipLaunchKernelGGL(k_expand_groups, eg, block, 0, st, ctx->d_vals[1], n, k == 64u ? ctx->d_queue : ctx->d_cost);
+                if (k == 64u) {  // whole groups, costliest first (coherent waves, longest chains first)
+                    b.queue = ctx->d_queue;
+                    hipLaunchKernelGGL(kern, dim3(blocks), block, lds, st, ctx->scene, b);
+                    HIPCHK(hipGetLastError());
+                    return NART_OK;
+                }
+                HIPCHK(hipMemcpyAsync(ctx->d_vals[1], ctx->d_cost, (size_t)n * 4, hipMemcpyDeviceToDevice, st));
+                // d_vals[1] = pixels by cost class; partition the rest (slot order) from the top k*W
+                hipLaunchKernelGGL(k_flag_top, eg, block, 0, st, ctx->d_vals[1], n, k * W, ctx->d_keys[0]);
+                hipLaunchKernelGGL(k_iota, eg, block, 0, st, ctx->d_cost, n);
+                tmp = ctx->cap_sort_tmp;
+                HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->d_sort_tmp, tmp, ctx->d_keys[0], ctx->d_keys[1],
+                                                          ctx->d_cost, ctx->d_vals[0], (int)n, 0, 1, st));
+                hipLaunchKernelGGL(k_build_queue, eg, block, 0, st, ctx->d_vals[1], ctx->d_vals[0], n, W, k,
+                                   ctx->d_queue);
+            }
+            b.queue = ctx->d_queue;
+            if (refill) {
+                HIPCHK(hipMemsetAsync(ctx->d_qhead, 0, sizeof(uint32_t), st));
+                b.qhead = ctx->d_qhead;
+                b.qbase = resident * 256;
+                blocks = resident;
+            }
+        }
+    }
+    hipLaunchKernelGGL(kern, dim3(blocks), block, lds, st, ctx->scene, b);
+    HIPCHK(hipGetLastError());
+    return NART_OK;
 }
 
 template <bool ENV>
-void launch_render_maxl(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
+int launch_render_maxl(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     const bool c = ctx->counters;
-    if (a.bounces <= 10) c ? launch_render<10, true, ENV>(ctx, a, st) : launch_render<10, false, ENV>(ctx, a, st);
-    else if (a.bounces <= 16) c ? launch_render<16, true, ENV>(ctx, a, st) : launch_render<16, false, ENV>(ctx, a, st);
-    else c ? launch_render<32, true, ENV>(ctx, a, st) : launch_render<32, false, ENV>(ctx, a, st);
+    if (a.bounces <= 10) return c ? launch_render<10, true, ENV>(ctx, a, st) : launch_render<10, false, ENV>(ctx, a, st);
+    if (a.bounces <= 16) return c ? launch_render<16, true, ENV>(ctx, a, st) : launch_render<16, false, ENV>(ctx, a, st);
+    return c ? launch_render<32, true, ENV>(ctx, a, st) : launch_render<32, false, ENV>(ctx, a, st);
 }
 
 int dispatch_megakernel(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
-    if (ctx->has_env) launch_render_maxl<true>(ctx, a, st);
-    else launch_render_maxl<false>(ctx, a, st);
-    HIPCHK(hipGetLastError());
-    return NART_OK;
+    return ctx->has_env ? launch_render_maxl<true>(ctx, a, st) : launch_render_maxl<false>(ctx, a, st);
 }
 
 // ---------------------------------------------------------------- wavefront variant
@@ -477,8 +651,13 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
     nart_filter_table(table);
     if (!ctx->d_table) HIPCHK(hipMalloc(&ctx->d_table, 64 * sizeof(float)));
     HIPCHK(hipMemcpyAsync(ctx->d_table, table, sizeof(table), hipMemcpyHostToDevice, st));
-    if (!ctx->d_counters) HIPCHK(hipMalloc(&ctx->d_counters, 8 * sizeof(unsigned long long)));
-    if (ctx->counters) HIPCHK(hipMemsetAsync(ctx->d_counters, 0, 8 * sizeof(unsigned long long), st));
+#ifdef NART_WAVEPROF
+    const size_t n_cnt = 24 + 8 * 70000 + 4200000;  // + per-wave and per-slot records (development profile)
+#else
+    const size_t n_cnt = 24;
+#endif
+    if (!ctx->d_counters) HIPCHK(hipMalloc(&ctx->d_counters, n_cnt * sizeof(unsigned long long)));
+    if (ctx->counters) HIPCHK(hipMemsetAsync(ctx->d_counters, 0, n_cnt * sizeof(unsigned long long), st));
     if (!ctx->events) {
         for (auto& e : ctx->ev) HIPCHK(hipEventCreate(&e));
         ctx->events = true;
@@ -533,6 +712,7 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         ra.lds_nodes = 0;
         ra.gamma = p->roughening_factor * p->roughening_factor;
         ra.counters = ctx->d_counters;
+        ra.sstride = p->spp;
         HIPCHK(hipEventRecord(ctx->ev[3], st));
         rc = launch_latin(ctx, ra, st);
         if (rc) return rc;
@@ -594,6 +774,46 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
             stats->bounces += c[4];
             stats->octree_checks += c[5];
             stats->octree_replays += c[6];
+#ifdef NART_WAVEPROF
+            unsigned long long w[24];
+            HIPCHK(hipMemcpy(w, ctx->d_counters, sizeof(w), hipMemcpyDeviceToHost));
+            {
+                const uint32_t nw = (uint32_t)std::min<size_t>((xy.size() + 63) / 64, 70000);
+                std::vector<unsigned long long> pw(8 * (size_t)nw);
+                HIPCHK(hipMemcpy(pw.data(), ctx->d_counters + 24, pw.size() * 8, hipMemcpyDeviceToHost));
+                std::vector<std::pair<unsigned long long, uint32_t>> cy;
+                for (uint32_t i = 0; i < nw; ++i) cy.push_back({pw[8 * i], i});
+                std::sort(cy.begin(), cy.end());
+                auto q = [&](double f) { return cy[(size_t)(f * (cy.size() - 1))].first; };
+                unsigned long long rp = 0, rp_top = 0;
+                for (uint32_t i = 0; i < nw; ++i) rp += pw[4 * i + 1];
+                for (size_t k = 0; k < cy.size() / 100; ++k) rp_top += pw[4 * cy[cy.size() - 1 - k].second + 1];
+                {
+                    const uint32_t m = cy[cy.size() / 2].second;
+                    fprintf(stderr, "WAVEPROF median wave cycles %llu trav %llu iterations %llu node-iters %llu/%llu tri-iters %llu/%llu\n",
+                            pw[8 * m], pw[8 * m + 1], pw[8 * m + 2], pw[8 * m + 4], pw[8 * m + 5], pw[8 * m + 6], pw[8 * m + 7]);
+                }
+                fprintf(stderr, "WAVEPROF waves %u cycles p10 %llu p50 %llu p90 %llu p99 %llu max %llu\n", nw, q(0.1), q(0.5),
+                        q(0.9), q(0.99), q(1.0));
+                for (size_t k = 0; k < 6 && k < cy.size(); ++k) {
+                    const uint32_t i = cy[cy.size() - 1 - k].second;
+                    const uint32_t s0 = (uint32_t)pw[8 * i + 3];
+                    fprintf(stderr, "WAVEPROF top wave %u cycles %llu trav-cycles %llu iterations %llu node-iters %llu/%llu tri-iters %llu/%llu px (%u,%u)\n", i, pw[8 * i],
+                            pw[8 * i + 1], pw[8 * i + 2], pw[8 * i + 4], pw[8 * i + 5], pw[8 * i + 6], pw[8 * i + 7], s0 < xy.size() ? xy[s0] & 0xFFFF : 0, s0 < xy.size() ? xy[s0] >> 16 : 0);
+                }
+            }
+            if (const char* dump = std::getenv("NART_WAVEPROF_DUMP")) {
+                std::vector<unsigned long long> ps(xy.size());
+                HIPCHK(hipMemcpy(ps.data(), ctx->d_counters + 24 + 8 * 70000, ps.size() * 8, hipMemcpyDeviceToHost));
+                if (FILE* f = fopen(dump, "wb")) {
+                    fwrite(xy.data(), 4, xy.size(), f);
+                    fwrite(ps.data(), 8, ps.size(), f);
+                    fclose(f);
+                }
+            }
+            fprintf(stderr, "WAVEPROF steps %llu/%llu nodes %llu/%llu tris %llu/%llu trav_cyc %llu total_cyc %llu shade %llu/%llu\n",
+                    w[8], w[9], w[10], w[11], w[12], w[13], w[14], w[15], w[16], w[17]);
+#endif
         }
     }
     return NART_OK;
@@ -754,7 +974,9 @@ void nart_hip_destroy(nart_ctx* ctx) {
     void* bufs[] = {ctx->d_nodes, ctx->d_tri_isect, ctx->d_tris, ctx->d_tri_mesh, ctx->d_meshes, ctx->d_mats,
                     ctx->d_lights, ctx->d_texs, ctx->d_tex_pool, ctx->d_slot_xy, ctx->d_rng, ctx->d_samples,
                     ctx->d_L, ctx->d_bucket_ids, ctx->d_bucket_base, ctx->d_table, ctx->d_counters, ctx->d_wf, ctx->d_envs, ctx->d_density,
-                    ctx->d_oc_nodes, ctx->d_oc_chunks, ctx->d_oc_tris, ctx->d_tri_leaf, ctx->d_oc_lock, ctx->d_oc_heap};
+                    ctx->d_oc_nodes, ctx->d_oc_chunks, ctx->d_oc_tris, ctx->d_tri_leaf, ctx->d_oc_lock, ctx->d_oc_heap,
+                    ctx->d_queue, ctx->d_cost, ctx->d_keys[0], ctx->d_keys[1], ctx->d_vals[0], ctx->d_vals[1],
+                    ctx->d_qhead, ctx->d_sort_tmp};
     for (void* b : bufs)
         if (b) hipFree(b);
     for (void* b : ctx->env_bufs) hipFree(b);
@@ -861,7 +1083,7 @@ int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t
     rc = ensure(ctx, n, p->spp, 1);
     if (rc) return rc;
     HIPCHK(hipMemcpy(ctx->d_slot_xy, xy.data(), (size_t)n * 4, hipMemcpyHostToDevice));
-    if (!ctx->d_counters) HIPCHK(hipMalloc(&ctx->d_counters, 8 * sizeof(unsigned long long)));
+    if (!ctx->d_counters) HIPCHK(hipMalloc(&ctx->d_counters, 24 * sizeof(unsigned long long)));
     RenderArgs ra;
     ra.slot_xy = ctx->d_slot_xy;
     ra.samples = ctx->d_samples;
@@ -877,6 +1099,7 @@ int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t
     ra.lds_nodes = 0;
     ra.gamma = p->roughening_factor * p->roughening_factor;
     ra.counters = ctx->d_counters;
+    ra.sstride = p->spp;
     rc = launch_latin(ctx, ra, 0);
     if (rc) return rc;
     rc = dispatch_render(ctx, ra, p->integrator, 0);

@@ -88,6 +88,24 @@ def test_framebuffer_glass_sphere_c1(glass_gpu, glass_oracle, glass_scene):
     assert np.isfinite(res).all()
 
 
+@pytest.mark.parametrize("w,h", [(1024, 576), (512, 400)], ids=["k32", "k8"])
+def test_queue_scheduler_frames(gpu, glass_scene, w, h):
+    """More traced pixels than resident lanes: the megakernel runs the cost probe, the costly
+    pixels are spread over the persistent waves and finished lanes refill from the queue
+    (render.hip launch_render).  Only the order of work changes; the frame must not."""
+    p = _params(glass_scene, w, h, 2)
+    g = nart_amd.HipRenderer(glass_scene, variant=0).render(p)
+    r = oracle.Oracle(glass_scene).render(p)
+    assert _bits_equal(g, r), _report(g, r)
+
+
+def test_queue_scheduler_environment(gpu, env_scene):
+    p = _params(env_scene, 480, 300, 2)
+    g = nart_amd.HipRenderer(env_scene, variant=0).render(p)
+    r = oracle.Oracle(env_scene).render(p)
+    assert _bits_equal(g, r), _report(g, r)
+
+
 def test_framebuffer_ragged_buckets(glass_gpu, glass_oracle, glass_scene):
     """Image not a multiple of the bucket size: extra traced rows/cols (render.cpp:164-168)."""
     p = _params(glass_scene, 50, 37, 3, bucket_size=16, filter_width=1.5, bounces=7)
