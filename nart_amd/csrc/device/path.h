@@ -167,8 +167,9 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
         float4 a, b, c;
         int4 k;
         if (t.code < nl) {
-#if !defined(NART_NODE_FLAT) && defined(__HIP_DEVICE_COMPILE__)
+#if defined(NART_NODE_DS) && defined(__HIP_DEVICE_COMPILE__)
             // explicit LDS address space: ds_read_b128, not a flat load through the generic aperture
+            // (opt-in: C3 full frame 577 vs 570 ms with the flat load)
             typedef float v4f __attribute__((ext_vector_type(4)));
             typedef const __attribute__((address_space(3))) v4f lds_v4f;
             lds_v4f* np = (lds_v4f*)lnodes + 4 * t.code;
@@ -221,16 +222,17 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
     }
     const uint32_t lc = ~(uint32_t)t.code;
     const uint32_t first = lc >> 5, count = (lc & 31u) + 1u;
-#ifndef NART_TRI_SERIAL
-    // software-pipelined leaf: the records of triangle i + 1 are in flight while triangle i is
-    // tested (the last iteration reloads its own record instead of reading past the leaf)
+#ifdef NART_TRI_PIPELINE
+    // Software-pipelined leaf: the records of triangle i + 1 are in flight while triangle i is
+    // tested; the last iteration reloads its own record instead of reading past the leaf.
+    // Opt-in: no faster on the C3 full frame.
     const float4* tp0 = S.tri_isect + 4 * first;
     float4 na = tp0[0], nb = tp0[1], nc = tp0[2], nd = tp0[3];
 #endif
     for (uint32_t i = 0; i < count; ++i) {
         if (COUNT) cnt.tris++;
         if (COUNT) WPROF(cnt, 4);
-#ifndef NART_TRI_SERIAL
+#ifdef NART_TRI_PIPELINE
         const float4 a = na, b = nb, c = nc, dd = nd;
         {
             const float4* tq = tp0 + 4 * (i + 1 < count ? i + 1 : i);
@@ -246,7 +248,7 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
         float e0, e1, e2;
         edge_functions(r, F3(b.x, b.y, b.z), F3(b.w, c.x, c.y), F3(c.z, c.w, dd.x), e0, e1, e2);
         if (!edges_accept(e0, e1, e2)) continue;
-#ifdef NART_TRI_SERIAL
+#ifndef NART_TRI_PIPELINE
         float4 a = tp[0];
 #endif
         f3 n = F3(a.x, a.y, a.z);
