@@ -131,7 +131,7 @@ ND bool maj_next(const DMedium& m, MajIter& it, float& sigma, float& t0, float& 
 
 // VolumeIntegrator::Li_alpha with SampleT_maj inlined (T_maj only feeds an unused callback
 // argument, so its exp() factors are not evaluated).
-ND f4 li_volume(const DScene& S, const RenderArgs& A, uint32_t& rng, f3 o, f3 d) {
+ND f4 li_volume(const DScene& S, const RenderArgs& A, uint32_t& rng, f3 o, f3 d, uint32_t& work) {
     const DMedium& m = S.medium;
     f3 L = F3(0.f, 0.f, 0.f);
     const f3 beta = F3(1.f, 1.f, 1.f);
@@ -149,6 +149,7 @@ ND f4 li_volume(const DScene& S, const RenderArgs& A, uint32_t& rng, f3 o, f3 d)
                 if (!maj_next(m, it, sigma, t0, t1)) break;
                 float tMin = t0;
                 for (;;) {
+                    ++work;  // tentative collisions: the cost probe's measure
                     const float t = tMin + (-glibc_logf(1.f - rng_float(rng)) / sigma);
                     if (!(t < t1)) break;
                     const f3 p = add(ro, muls(rd, t));
@@ -206,20 +207,29 @@ ND f4 li_volume(const DScene& S, const RenderArgs& A, uint32_t& rng, f3 o, f3 d)
     return F4(L.x, L.y, L.z, 1.f);
 }
 
+// One lane per traced pixel.  With A.queue the launch order of pixels is the queue's (the
+// scheduler puts the costliest wave-sized groups first, render.hip dispatch_volume); with
+// A.cost the kernel is the cost probe (tentative collisions of the pixel's first samples).
 template <bool COUNT>
 __global__ __launch_bounds__(256) void k_render_volume(DScene S, RenderArgs A) {
-    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
-    if (slot >= A.n_slots) return;
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= A.n_slots) return;
+    const uint32_t slot = A.queue ? A.queue[gid] : gid;
     const uint32_t xy = A.slot_xy[slot];
     const uint32_t px = xy & 0xFFFFu, py = xy >> 16;
     uint32_t rng = A.rng0[slot];
-    const float2* smp = A.samples + (size_t)slot * A.spp;
-    float4* out = A.Lout + (size_t)slot * A.spp;
+    const float2* smp = A.samples + (size_t)slot * A.sstride;
+    float4* out = A.Lout + (size_t)slot * A.sstride;
+    uint32_t work = 0;
     for (uint32_t s = 0; s < A.spp; ++s) {
         const float2 sm = smp[s];
         const Ray r = cast_ray(S, F2(sm.x, sm.y), A.W, A.H, px, py);
-        const f4 L = li_volume(S, A, rng, r.o, r.d);
+        const f4 L = li_volume(S, A, rng, r.o, r.d, work);
         out[s] = make_float4(L.x, L.y, L.z, L.w);
+    }
+    if (A.cost) {
+        A.cost[gid] = work + A.spp;
+        return;
     }
     if (COUNT) atomicAdd(&A.counters[0], (unsigned long long)A.spp);
 }

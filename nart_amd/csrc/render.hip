@@ -393,6 +393,10 @@ __global__ void k_build_queue(const uint32_t* top, const uint32_t* rest, uint32_
     }
 }
 
+// Pixel list (into `out`) of the wave-sized slot groups ordered by the probe costs in
+// ctx->d_cost, costliest group first (ties keep slot order).
+int sort_groups_by_cost(nart_ctx* ctx, uint32_t n, uint32_t* out, hipStream_t st);
+
 __global__ void k_iota(uint32_t* v, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) v[i] = i;
@@ -405,6 +409,18 @@ int queue_mode() {
         m = e ? std::max(0, std::min(2, std::atoi(e))) : 2;
     }
     return m;
+}
+
+int sort_groups_by_cost(nart_ctx* ctx, uint32_t n, uint32_t* out, hipStream_t st) {
+    const uint32_t ng = (n + 63) / 64;
+    hipLaunchKernelGGL(k_group_keys, dim3((ng + 255) / 256), dim3(256), 0, st, ctx->d_cost, n, ctx->d_keys[0],
+                       ctx->d_vals[0]);
+    size_t tmp = ctx->cap_sort_tmp;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->d_sort_tmp, tmp, ctx->d_keys[0], ctx->d_keys[1], ctx->d_vals[0],
+                                              ctx->d_vals[1], (int)ng, 0, 32, st));
+    hipLaunchKernelGGL(k_expand_groups, dim3((n + 255) / 256), dim3(256), 0, st, ctx->d_vals[1], n, out);
+    HIPCHK(hipGetLastError());
+    return NART_OK;
 }
 
 template <int MAXL, bool COUNT, bool ENV>
@@ -454,13 +470,9 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                 pb.spp = 1;
                 pb.cost = ctx->d_cost;
                 hipLaunchKernelGGL((k_render<MAXL, true, ENV>), dim3(blocks), block, lds, st, ctx->scene, pb);
-                const uint32_t ng = (n + 63) / 64;
-                hipLaunchKernelGGL(k_group_keys, dim3((ng + 255) / 256), block, 0, st, ctx->d_cost, n, ctx->d_keys[0],
-                                   ctx->d_vals[0]);
-                size_t tmp = ctx->cap_sort_tmp;
-                HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->d_sort_tmp, tmp, ctx->d_keys[0], ctx->d_keys[1],
-                                                          ctx->d_vals[0], ctx->d_vals[1], (int)ng, 0, 32, st));
-                hipLaunchKernelGGL(k_expand_groups, eg, block, 0, st, ctx->d_vals[1], n, k == 64u ? ctx->d_queue : ctx->d_cost);
+                int rc2 = sort_groups_by_cost(ctx, n, k == 64u ? ctx->d_queue : ctx->d_cost, st);
+                if (rc2) return rc2;
+                size_t tmp = 0;
                 if (k == 64u) {  // whole groups, costliest first (coherent waves, longest chains first)
                     b.queue = ctx->d_queue;
                     hipLaunchKernelGGL(kern, dim3(blocks), block, lds, st, ctx->scene, b);
@@ -611,10 +623,34 @@ int dispatch_wavefront(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     return c ? run_wavefront<32, true>(ctx, a, st) : run_wavefront<32, false>(ctx, a, st);
 }
 
+// Volume integrator.  Its lanes run each sample to completion in lock step, so a wave costs
+// the sum over samples of its slowest lane and refilling single lanes would not help; when the
+// shard spans several rounds of resident waves, the costliest wave-sized pixel groups (cost
+// probe: tentative collisions of 4 samples per pixel) are launched first.
 int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
-    dim3 grid((a.n_slots + 255) / 256), block(256);
-    if (ctx->counters) hipLaunchKernelGGL((k_render_volume<true>), grid, block, 0, st, ctx->scene, a);
-    else hipLaunchKernelGGL((k_render_volume<false>), grid, block, 0, st, ctx->scene, a);
+    const dim3 block(256);
+    const uint32_t blocks = (a.n_slots + 255) / 256;
+    RenderArgs b = a;
+    if (queue_mode() == 2) {
+        int cus = 0, per_cu = 0;
+        HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_render_volume<false>, 256, 0));
+        const uint32_t resident = (uint32_t)std::max(1, cus * std::max(per_cu, 1));
+        const uint32_t n = a.n_slots;
+        if (blocks > resident && (double)n / (256.0 * resident) < 12.0 && a.spp > 4) {
+            int rc = ensure_queue(ctx, n);
+            if (rc) return rc;
+            RenderArgs pb = a;
+            pb.spp = 4;
+            pb.cost = ctx->d_cost;
+            hipLaunchKernelGGL((k_render_volume<false>), dim3(blocks), block, 0, st, ctx->scene, pb);
+            rc = sort_groups_by_cost(ctx, n, ctx->d_queue, st);
+            if (rc) return rc;
+            b.queue = ctx->d_queue;
+        }
+    }
+    if (ctx->counters) hipLaunchKernelGGL((k_render_volume<true>), dim3(blocks), block, 0, st, ctx->scene, b);
+    else hipLaunchKernelGGL((k_render_volume<false>), dim3(blocks), block, 0, st, ctx->scene, b);
     HIPCHK(hipGetLastError());
     return NART_OK;
 }

@@ -171,6 +171,16 @@ def test_volume_integrator(gpu, volume_scenes, kind):
     assert _bits_equal(g, r), _report(g, r)
 
 
+def test_volume_queue_scheduler(gpu, volume_scenes):
+    """More pixels than resident lanes: the volume kernel runs its cost probe (4 samples per
+    pixel) and launches the costliest pixel groups first (render.hip dispatch_volume)."""
+    sc = volume_scenes["c5"]
+    p = _params(sc, 640, 360, 8)
+    g = nart_amd.HipRenderer(sc).render(p)
+    r = oracle.Oracle(sc).render(p)
+    assert _bits_equal(g, r), _report(g, r)
+
+
 def test_volume_per_sample(gpu, volume_scenes):
     sc = volume_scenes["c5"]
     p = _params(sc, 320, 180, 32)

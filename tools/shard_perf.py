@@ -24,14 +24,19 @@ from nart_amd.dist import BucketShard  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ns", type=int, nargs="+", default=[1, 2, 4, 8])
-    ap.add_argument("-s", type=int, default=256)
+    ap.add_argument("-s", type=int, default=0)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--rank", type=int, default=-1, help="-1: every rank of each N (max reported)")
+    ap.add_argument("--config", default="c3", help="bench.py config (c2, c3, c4, c5); -s overrides its spp")
     a = ap.parse_args()
-    path = scenes.glass_sphere(os.path.join("/tmp", "nart_shard_%d" % os.getpid()))
+    sys.path.insert(0, REPO)
+    import bench
+    cfg = bench.CONFIGS[a.config]
+    path = cfg["scene"](os.path.join("/tmp", "nart_shard_%d" % os.getpid()))
     scene = nart_amd.Scene(path)
     p = nart_amd.load_sessions(path)[0]
-    p.image_width, p.image_height, p.spp = 1920, 1080, a.s
+    p.image_width, p.image_height = cfg["w"], cfg["h"]
+    p.spp = a.s if a.s > 0 else cfg["spp"]
     g = nart_amd.session_geometry(p)
     nb = g.n_buckets_x * g.n_buckets_y
     tpx = g.tile_size * g.tile_size
