@@ -79,6 +79,11 @@ int nart_hip_set_counters(nart_ctx* ctx, int enable);
 /* Device self-test: glibc-equivalent sinf/cosf over n inputs (parity of the device libm). */
 int nart_hip_eval_sincos(nart_ctx* ctx, const float* x, uint32_t n, float* sin_out, float* cos_out);
 
+/* Splat filter-index thresholds (host only, no device): thr65[k] = the least d2 whose AddSample
+   filter index (render.cpp:43-49) is >= k.  NART_E_INVALID when filter_width is too small for
+   them (the splat then evaluates sqrt and division per pair). */
+int nart_hip_splat_thresholds(float filter_width, float* thr65);
+
 /* Kernel variant: 0 = megakernel (one lane per pixel slot), 1 = wavefront (ray queues). */
 int nart_hip_set_variant(nart_ctx* ctx, int variant);
 

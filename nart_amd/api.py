@@ -97,6 +97,7 @@ _HIP_SIGS = {
     "nart_hip_set_counters": (ctypes.c_int, [_P, ctypes.c_int]),
     "nart_hip_eval_sincos": (ctypes.c_int, [_P, _P, ctypes.c_uint32, _P, _P]),
     "nart_hip_set_variant": (ctypes.c_int, [_P, ctypes.c_int]),
+    "nart_hip_splat_thresholds": (ctypes.c_int, [ctypes.c_float, _P]),
 }
 SCENE_SYMBOLS = tuple(_SCENE_SIGS)
 HIP_SYMBOLS = tuple(_HIP_SIGS)

@@ -78,9 +78,13 @@ ND Ray cast_ray(const DScene& S, f2 smp, uint32_t W, uint32_t H, uint32_t x, uin
 
 struct RenderArgs {
     const uint32_t* slot_xy;  // traced pixel (x | y << 16) in image coordinates
-    const float2* samples;    // [slot][spp] LatinSquare image samples
+    const float2* samples;    // LatinSquare image samples, sample s of slot at slot_so (sample_index)
     const uint32_t* rng0;     // [slot] RNG state after the LatinSquare
-    float4* Lout;             // [slot][spp] Li_alpha
+    float4* Lout;             // Li_alpha, same indexing as samples
+    // [slot] {first sample index, sample stride}.  Bucket renders lay each bucket out sample-major
+    // ([bucket][s][pixel of bucket]: the splat's lanes then read neighbouring pixels' sample s
+    // from one cache line); the per-sample API uses {slot * spp, 1}.
+    const uint2* slot_so;
     uint32_t n_slots, spp, bounces, W, H, totalW, stack_depth;
     float gamma;              // roughening factor squared (pathintegrator.cpp:163)
     unsigned long long* counters;  // [5] extend rays, shadow rays, node visits, tri tests, bounces
@@ -91,8 +95,12 @@ struct RenderArgs {
     uint32_t* qhead = nullptr;
     uint32_t qbase = 0;
     uint32_t* cost = nullptr; // cost probe: per-slot work estimate of the rendered sample(s)
-    uint32_t sstride = 0;     // per-slot stride of samples / Lout (= spp except in the cost probe)
 };
+
+ND uint32_t sample_index(const RenderArgs& A, uint32_t slot, uint32_t s) {
+    const uint2 so = A.slot_so[slot];
+    return so.x + s * so.y;
+}
 
 // Stage the top BVH nodes (breadth-first prefix) into LDS; every thread of the block calls it.
 ND void stage_nodes(const DScene& S, float4* dst, uint32_t n) {
@@ -108,23 +116,24 @@ __global__ __launch_bounds__(256) void k_latin(RenderArgs A) {
     uint32_t xy = A.slot_xy[slot];
     uint32_t x = xy & 0xFFFFu, y = xy >> 16;
     uint32_t rng = (y * A.totalW + x) + 2463534242u;  // RNG::Seed (rng.h:10-13)
-    float2* s = const_cast<float2*>(A.samples) + (size_t)slot * A.spp;
-    const uint32_t n = A.spp;
+    const uint2 so = A.slot_so[slot];
+    float2* s = const_cast<float2*>(A.samples) + so.x;
+    const uint32_t n = A.spp, st = so.y;
     const float inv = 1.f / (float)n;
     for (uint32_t i = 0; i < n; ++i) {
         float a = ((float)i + rng_float(rng)) * inv;  // StratifiedSample1D, x drawn first (Q2)
         float b = ((float)i + rng_float(rng)) * inv;
-        s[i] = make_float2(a, b);
+        s[i * st] = make_float2(a, b);
     }
     for (uint32_t i = 0; i < n; ++i) {
         uint32_t c = rng_int(rng, n - 1 - i);
-        float t = s[i].x;
-        s[i].x = s[c].x;
-        s[c].x = t;
+        float t = s[i * st].x;
+        s[i * st].x = s[c * st].x;
+        s[c * st].x = t;
         c = rng_int(rng, n - 1 - i);
-        t = s[i].y;
-        s[i].y = s[c].y;
-        s[c].y = t;
+        t = s[i * st].y;
+        s[i * st].y = s[c * st].y;
+        s[c * st].y = t;
     }
     const_cast<uint32_t*>(A.rng0)[slot] = rng;
 }
@@ -157,8 +166,85 @@ __global__ __launch_bounds__(64) void k_latin_lds(RenderArgs A) {
         ys[i * 64] = ys[c * 64];
         ys[c * 64] = t;
     }
-    float2* s = const_cast<float2*>(A.samples) + (size_t)slot * n;
-    for (uint32_t i = 0; i < n; ++i) s[i] = make_float2(xs[i * 64], ys[i * 64]);
+    const uint2 so = A.slot_so[slot];
+    float2* s = const_cast<float2*>(A.samples) + so.x;
+    for (uint32_t i = 0; i < n; ++i) s[i * so.y] = make_float2(xs[i * 64], ys[i * 64]);
+    const_cast<uint32_t*>(A.rng0)[slot] = rng;
+}
+
+// The same LatinSquare for 256 < spp <= 1024, where two float arrays per lane no longer fit in
+// LDS.  The shuffles only move values, so they are replayed on 16-bit stratum indices in LDS
+// ([spp][64 lanes]); the jittered stratum values are written once to a scratch area (the Lout
+// buffer, which k_render fills later) laid out [block][stratum][lane], and gathered through the
+// final indices.  Both index arrays share the LDS when 4*spp*64 bytes fit (spp <= 512); above
+// that the x and y shuffles run as two passes over the same RNG draws.
+__global__ __launch_bounds__(64) void k_latin_idx(RenderArgs A, float* scratch) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t s_idx[];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t slot = blockIdx.x * 64 + lane;
+    if (slot >= A.n_slots) return;
+    const uint32_t n = A.spp;
+    const bool both = n <= 512u;
+    const uint32_t xy = A.slot_xy[slot];
+    const uint32_t x = xy & 0xFFFFu, y = xy >> 16;
+    uint32_t rng = (y * A.totalW + x) + 2463534242u;
+    const float inv = 1.f / (float)n;
+    float* vx = scratch + (size_t)blockIdx.x * 2 * n * 64 + lane;  // [stratum][lane]
+    float* vy = vx + (size_t)n * 64;
+    for (uint32_t i = 0; i < n; ++i) {
+        vx[(size_t)i * 64] = ((float)i + rng_float(rng)) * inv;  // StratifiedSample1D, x drawn first (Q2)
+        vy[(size_t)i * 64] = ((float)i + rng_float(rng)) * inv;
+    }
+    const uint32_t rng_gen = rng;
+    const uint2 so = A.slot_so[slot];
+    float2* s = const_cast<float2*>(A.samples) + so.x;
+    uint16_t* ix = s_idx + lane;
+    uint16_t* iy = s_idx + (size_t)n * 64 + lane;
+    for (int pass = 0; pass < (both ? 1 : 2); ++pass) {
+        rng = rng_gen;
+        const bool dx = both || pass == 0, dy = both || pass == 1;
+        uint16_t* jy = both ? iy : ix;  // single-array passes reuse the first index array
+        for (uint32_t i = 0; i < n; ++i) {
+            if (dx) ix[i * 64] = (uint16_t)i;
+            if (dy) jy[i * 64] = (uint16_t)i;
+        }
+        for (uint32_t i = 0; i < n; ++i) {
+            uint32_t c = rng_int(rng, n - 1 - i);
+            if (dx) {
+                const uint16_t t = ix[i * 64];
+                ix[i * 64] = ix[c * 64];
+                ix[c * 64] = t;
+            }
+            c = rng_int(rng, n - 1 - i);
+            if (dy) {
+                const uint16_t t = jy[i * 64];
+                jy[i * 64] = jy[c * 64];
+                jy[c * 64] = t;
+            }
+        }
+        // gathers in groups of 16 (tail below), so that
+        // one wave per CU keeps 16-32 scratch loads in flight instead of one
+        uint32_t i = 0;
+        for (; i + 16 <= n; i += 16) {
+            float gx[16], gy[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                if (dx) gx[u] = vx[(size_t)ix[(i + u) * 64] * 64];
+                if (dy) gy[u] = vy[(size_t)jy[(i + u) * 64] * 64];
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                if (both) s[(i + u) * so.y] = make_float2(gx[u], gy[u]);
+                else if (dx) s[(i + u) * so.y].x = gx[u];
+                else s[(i + u) * so.y].y = gy[u];
+            }
+        }
+        for (; i < n; ++i) {
+            if (both) s[i * so.y] = make_float2(vx[(size_t)ix[i * 64] * 64], vy[(size_t)iy[i * 64] * 64]);
+            else if (dx) s[i * so.y].x = vx[(size_t)ix[i * 64] * 64];
+            else s[i * so.y].y = vy[(size_t)ix[i * 64] * 64];
+        }
+    }
     const_cast<uint32_t*>(A.rng0)[slot] = rng;
 }
 
@@ -202,7 +288,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
     } else if (slot >= A.n_slots) {
         return;
     }
-    uint32_t px = 0, py = 0, rng = 0;
+    uint32_t px = 0, py = 0, rng = 0, soff = 0, sstr = 0;
     const float2* smp = A.samples;
     float4* out = A.Lout;
     auto take_pixel = [&](uint32_t sl) {
@@ -211,8 +297,9 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
         px = xy & 0xFFFFu;
         py = xy >> 16;
         rng = A.rng0[sl];
-        smp = A.samples + (size_t)sl * A.sstride;
-        out = A.Lout + (size_t)sl * A.sstride;
+        const uint2 so = A.slot_so[sl];
+        soff = so.x;
+        sstr = so.y;
     };
     if (slot != 0xFFFFFFFFu) take_pixel(slot);
     int* sc = s_code + tid;
@@ -269,7 +356,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
         ++iters;
         if (new_sample) {
             if (s >= A.spp) break;
-            float2 sm = smp[s];
+            float2 sm = smp[soff + s * sstr];
             ray = cast_ray(S, F2(sm.x, sm.y), A.W, A.H, px, py);
             L = F3(0.f, 0.f, 0.f);
             alpha = 0.f;
@@ -288,7 +375,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
         if (new_bounce) {
             new_bounce = false;
             if (bounce >= A.bounces) {
-                out[s] = make_float4(L.x, L.y, L.z, alpha);
+                out[soff + s * sstr] = make_float4(L.x, L.y, L.z, alpha);
                 ++s;
                 new_sample = true;
                 continue;
@@ -347,7 +434,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
                 // escaped: at bounce 0 the light seen directly is the result; at bounce > 0 the
                 // reference repeats the same miss until the loop ends (no RNG, no state change)
                 if (bounce == 0 && lightHit) L = Le;
-                out[s] = make_float4(L.x, L.y, L.z, alpha);
+                out[soff + s * sstr] = make_float4(L.x, L.y, L.z, alpha);
                 ++s;
                 new_sample = true;
                 continue;
@@ -491,7 +578,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
                 ray = nxt;
                 new_bounce = true;
             } else {
-                out[s] = make_float4(L.x, L.y, L.z, alpha);
+                out[soff + s * sstr] = make_float4(L.x, L.y, L.z, alpha);
                 ++s;
                 new_sample = true;
             }
@@ -543,10 +630,12 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
 struct SplatArgs {
     const uint32_t* bucket_ids;   // [n_buckets] bucket id = by * nbx + bx
     const uint32_t* bucket_base;  // [n_buckets] first slot of each bucket
-    const float2* samples;        // [slot][spp]
-    const float4* Lout;           // [slot][spp]
+    const float2* samples;        // sample-major per bucket (RenderArgs::slot_so)
+    const float4* Lout;           // same layout
     float* tiles;                 // [n_buckets][tile*tile][5] (nart_pixel AoS)
     const float* table;           // [64] Gaussian filter table
+    const float* thr;             // [65] filter-index thresholds on d2 (splat_thresholds), or null
+    float idx_scale;              // 64 / fw: the estimate of the filter index that thr corrects
     uint32_t n_buckets, spp, B, fb, tile, nbx, totalW, totalH;
     float fw;
     float invB, invFw;            // exact reciprocals when B / fw are powers of two, else 0
@@ -583,10 +672,38 @@ ND bool splat_hits(const SplatArgs& A, const float* table, float scx, float scy,
     return hit;
 }
 
+// splat_hits with the filter index taken from the d2 thresholds: a hardware sqrt estimates the
+// index within one step and two threshold compares make it exact (no correctly rounded sqrt and
+// division per pair).
+ND bool splat_hits_thr(const SplatArgs& A, const float* table, const float* thr, float scx, float scy, uint32_t tx,
+                       uint32_t ty, float& w) {
+    const float fw = A.fw, fb = (float)A.fb, Bf = (float)A.B;
+    const uint32_t x0 = (uint32_t)floorf(scx - fw), x1 = (uint32_t)ceilf(scx + fw);
+    const uint32_t y0 = (uint32_t)floorf(scy - fw), y1 = (uint32_t)ceilf(scy + fw);
+    const uint32_t kx = (uint32_t)floorf(div_exact(scx - fb, Bf, A.invB));
+    const uint32_t ky = (uint32_t)floorf(div_exact(scy - fb, Bf, A.invB));
+    const uint32_t xs = tx + A.B * kx, ys = ty + A.B * ky;
+    const bool hit = xs >= x0 && xs < x1 && ys >= y0 && ys < y1;
+    const float distX = ((float)xs + 0.5f) - scx;
+    const float distY = ((float)ys + 0.5f) - scy;
+    const float d2 = distX * distX + distY * distY;
+    int g = (int)(__builtin_amdgcn_sqrtf(d2) * A.idx_scale);
+    g = g < 0 ? 0 : (g > 63 ? 63 : g);
+    const float t0 = thr[g], t1 = thr[g + 1];
+    const int fi = g - (d2 < t0 ? 1 : 0) + (d2 >= t1 ? 1 : 0);
+    w = table[fi];
+    return hit;
+}
+
+template <bool THR>
 __global__ __launch_bounds__(256) void k_splat(SplatArgs A) {
     __shared__ float s_table[64];
+    __shared__ float s_thr[65];
     if (threadIdx.x < 64) s_table[threadIdx.x] = A.table[threadIdx.x];
+    if (THR && threadIdx.x < 65) s_thr[threadIdx.x] = A.thr[threadIdx.x];
     __syncthreads();
+#define NART_SPLAT_HITS(scx, scy, w) \
+    (THR ? splat_hits_thr(A, s_table, s_thr, scx, scy, tx, ty, w) : splat_hits(A, s_table, scx, scy, tx, ty, w))
     const uint32_t tpx = A.tile * A.tile;
     const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (uint64_t)A.n_buckets * tpx) return;
@@ -597,6 +714,7 @@ __global__ __launch_bounds__(256) void k_splat(SplatArgs A) {
     const uint32_t x0 = A.B * bx, y0 = A.B * by;
     const uint32_t x1 = min(A.B * (bx + 1), A.totalW), y1 = min(A.B * (by + 1), A.totalH);
     const int bw = (int)(x1 - x0), bh = (int)(y1 - y0);
+    const uint32_t npx = (uint32_t)(bw * bh);
     const uint32_t base = A.bucket_base[bi];
     // Candidate source pixels.  A sample of bucket-local column S has sc - x0 in [S+fb, S+fb+1],
     // so its splat columns span [S+fb-ceil(fw), S+fb+1+fw): tile column tx can only be reached
@@ -616,30 +734,53 @@ __global__ __launch_bounds__(256) void k_splat(SplatArgs A) {
         for (int ci = 0; ci < ncol; ++ci) {
             const int sx = (sxlo + ci <= sxhi) ? sxlo + ci : bw - 1;
             const float fx = (float)(x0 + (uint32_t)sx + A.fb);
-            const uint64_t slot = base + (uint64_t)sy * bw + sx;
-            const float2* sp = A.samples + slot * A.spp;
-            const float4* lp = A.Lout + slot * A.spp;
+            // sample-major bucket layout (RenderArgs::slot_so): sample i of local pixel q at
+            // base*spp + i*npx + q, so lanes on neighbouring source pixels share cache lines
+            const uint64_t first = (uint64_t)base * A.spp + (uint32_t)(sy * bw + sx);
+            const float2* sp = A.samples + first;
+            const float4* lp = A.Lout + first;
             uint32_t i = 0;
             // 4 samples per step: all loads issued up front, adds applied in sample order
-            for (; (A.spp & 1u) == 0 && i + 4 <= A.spp; i += 4) {
-                float4 uv01 = *reinterpret_cast<const float4*>(sp + i);
-                float4 uv23 = *reinterpret_cast<const float4*>(sp + i + 2);
-                float4 L0 = lp[i], L1 = lp[i + 1], L2 = lp[i + 2], L3 = lp[i + 3];
+#ifndef NART_SPLAT_PF
+#define NART_SPLAT_PF 1
+#endif
+#if NART_SPLAT_PF
+            // software pipelined: the next 4 samples are in flight while these 4 are splatted
+            float2 nu0, nu1, nu2, nu3;
+            float4 nL0, nL1, nL2, nL3;
+            if (A.spp >= 4) {
+                nu0 = sp[0], nu1 = sp[npx], nu2 = sp[2 * npx], nu3 = sp[3 * npx];
+                nL0 = lp[0], nL1 = lp[npx], nL2 = lp[2 * npx], nL3 = lp[3 * npx];
+            }
+            for (; i + 4 <= A.spp; i += 4) {
+                const float2 uv0 = nu0, uv1 = nu1, uv2 = nu2, uv3 = nu3;
+                const float4 L0 = nL0, L1 = nL1, L2 = nL2, L3 = nL3;
+                if (i + 8 <= A.spp) {
+                    const size_t k0 = (size_t)(i + 4) * npx;
+                    nu0 = sp[k0], nu1 = sp[k0 + npx], nu2 = sp[k0 + 2 * npx], nu3 = sp[k0 + 3 * npx];
+                    nL0 = lp[k0], nL1 = lp[k0 + npx], nL2 = lp[k0 + 2 * npx], nL3 = lp[k0 + 3 * npx];
+                }
+#else
+            for (; i + 4 <= A.spp; i += 4) {
+                const size_t k0 = (size_t)i * npx;
+                float2 uv0 = sp[k0], uv1 = sp[k0 + npx], uv2 = sp[k0 + 2 * npx], uv3 = sp[k0 + 3 * npx];
+                float4 L0 = lp[k0], L1 = lp[k0 + npx], L2 = lp[k0 + 2 * npx], L3 = lp[k0 + 3 * npx];
+#endif
                 float w0, w1, w2, w3;
-                bool h0 = splat_hits(A, s_table, fx + uv01.x, fy + uv01.y, tx, ty, w0);
-                bool h1 = splat_hits(A, s_table, fx + uv01.z, fy + uv01.w, tx, ty, w1);
-                bool h2 = splat_hits(A, s_table, fx + uv23.x, fy + uv23.y, tx, ty, w2);
-                bool h3 = splat_hits(A, s_table, fx + uv23.z, fy + uv23.w, tx, ty, w3);
+                bool h0 = NART_SPLAT_HITS(fx + uv0.x, fy + uv0.y, w0);
+                bool h1 = NART_SPLAT_HITS(fx + uv1.x, fy + uv1.y, w1);
+                bool h2 = NART_SPLAT_HITS(fx + uv2.x, fy + uv2.y, w2);
+                bool h3 = NART_SPLAT_HITS(fx + uv3.x, fy + uv3.y, w3);
                 if (h0) { c0 += L0.x * w0; c1 += L0.y * w0; c2 += L0.z * w0; c3 += L0.w * w0; ws += w0; }
                 if (h1) { c0 += L1.x * w1; c1 += L1.y * w1; c2 += L1.z * w1; c3 += L1.w * w1; ws += w1; }
                 if (h2) { c0 += L2.x * w2; c1 += L2.y * w2; c2 += L2.z * w2; c3 += L2.w * w2; ws += w2; }
                 if (h3) { c0 += L3.x * w3; c1 += L3.y * w3; c2 += L3.z * w3; c3 += L3.w * w3; ws += w3; }
             }
             for (; i < A.spp; ++i) {
-                float2 uv = sp[i];
+                float2 uv = sp[(size_t)i * npx];
                 float w;
-                if (splat_hits(A, s_table, fx + uv.x, fy + uv.y, tx, ty, w)) {
-                    float4 Lv = lp[i];
+                if (NART_SPLAT_HITS(fx + uv.x, fy + uv.y, w)) {
+                    float4 Lv = lp[(size_t)i * npx];
                     c0 += Lv.x * w;
                     c1 += Lv.y * w;
                     c2 += Lv.z * w;
@@ -649,6 +790,7 @@ __global__ __launch_bounds__(256) void k_splat(SplatArgs A) {
             }
         }
     }
+#undef NART_SPLAT_HITS
     float* o = A.tiles + ((uint64_t)bi * tpx + tp) * 5;
     o[0] = c0;
     o[1] = c1;

@@ -218,14 +218,15 @@ __global__ __launch_bounds__(256) void k_render_volume(DScene S, RenderArgs A) {
     const uint32_t xy = A.slot_xy[slot];
     const uint32_t px = xy & 0xFFFFu, py = xy >> 16;
     uint32_t rng = A.rng0[slot];
-    const float2* smp = A.samples + (size_t)slot * A.sstride;
-    float4* out = A.Lout + (size_t)slot * A.sstride;
+    const uint2 so = A.slot_so[slot];
+    const float2* smp = A.samples + so.x;
+    float4* out = A.Lout + so.x;
     uint32_t work = 0;
     for (uint32_t s = 0; s < A.spp; ++s) {
-        const float2 sm = smp[s];
+        const float2 sm = smp[s * so.y];
         const Ray r = cast_ray(S, F2(sm.x, sm.y), A.W, A.H, px, py);
         const f4 L = li_volume(S, A, rng, r.o, r.d, work);
-        out[s] = make_float4(L.x, L.y, L.z, L.w);
+        out[s * so.y] = make_float4(L.x, L.y, L.z, L.w);
     }
     if (A.cost) {
         A.cost[gid] = work + A.spp;

@@ -89,7 +89,7 @@ ND uint32_t wave_sum(uint32_t v) {
 ND void gen_camera(const DScene& S, const RenderArgs& A, uint32_t slot, uint32_t s, f3& o, f3& d, float& tmax,
                    f3& Le, bool& lightHit) {
     const uint32_t xy = A.slot_xy[slot];
-    const float2 sm = A.samples[(size_t)slot * A.spp + s];
+    const float2 sm = A.samples[sample_index(A, slot, s)];
     Ray r = cast_ray(S, F2(sm.x, sm.y), A.W, A.H, xy & 0xFFFFu, xy >> 16);
     o = r.o;
     d = r.d;
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(256) void k_wf_init(DScene S, WFArgs A) {
         const bool live = slot < R.n_slots && R.bounces > 0;
         if (slot < R.n_slots && R.bounces == 0) {
             // every sample ends before its first light loop (pathintegrator.cpp:165)
-            for (uint32_t s = 0; s < R.spp; ++s) R.Lout[(size_t)slot * R.spp + s] = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (uint32_t s = 0; s < R.spp; ++s) R.Lout[sample_index(R, slot, s)] = make_float4(0.f, 0.f, 0.f, 0.f);
             A.st.u[slot] = make_uint4(0u, R.spp, 0u, WF_DEAD);
         }
         if (live) {
@@ -269,7 +269,7 @@ ND uint32_t shade_slot(const DScene& S, const WFArgs& A, uint32_t slot, const ui
     }
     // (b) the sample that ended last bounce is complete: store it, start the traced one
     if (fl & WF_FINISH) {
-        R.Lout[(size_t)slot * R.spp + s] = make_float4(L.x, L.y, L.z, alpha);
+        R.Lout[sample_index(R, slot, s)] = make_float4(L.x, L.y, L.z, alpha);
         ++s;
         if (fl & WF_RETIRE) {  // pixel done
             T.u[slot] = make_uint4(rng, s, bounce, WF_DEAD);
@@ -445,7 +445,7 @@ ND uint32_t shade_slot(const DScene& S, const WFArgs& A, uint32_t slot, const ui
                 fl |= WF_RETIRE;
             }
         } else {
-            R.Lout[(size_t)slot * R.spp + s] = make_float4(L.x, L.y, L.z, alpha);
+            R.Lout[sample_index(R, slot, s)] = make_float4(L.x, L.y, L.z, alpha);
             ++s;
             if (s >= R.spp) {  // pixel done
                 T.u[slot] = make_uint4(rng, s, bounce, WF_DEAD);

@@ -51,6 +51,7 @@ struct nart_ctx {
     // work buffers
     size_t cap_slot_bytes = 0, cap_misc = 0;
     uint32_t* d_slot_xy = nullptr;
+    uint2* d_slot_so = nullptr;  // [slot] {first sample index, sample stride} (RenderArgs::slot_so)
     uint32_t* d_rng = nullptr;
     float2* d_samples = nullptr;
     float4* d_L = nullptr;
@@ -275,9 +276,12 @@ int ensure(nart_ctx* ctx, size_t slots, uint32_t spp, size_t buckets) {
     if (slots > ctx->cap_slots) {
         if (ctx->d_slot_xy) hipFree(ctx->d_slot_xy);
         if (ctx->d_rng) hipFree(ctx->d_rng);
+        if (ctx->d_slot_so) hipFree(ctx->d_slot_so);
         ctx->d_slot_xy = nullptr;
         ctx->d_rng = nullptr;
+        ctx->d_slot_so = nullptr;
         HIPCHK(hipMalloc(&ctx->d_slot_xy, slots * 4));
+        HIPCHK(hipMalloc(&ctx->d_slot_so, slots * sizeof(uint2)));
         HIPCHK(hipMalloc(&ctx->d_rng, slots * 4));
         ctx->cap_slots = slots;
     }
@@ -396,6 +400,19 @@ __global__ void k_build_queue(const uint32_t* top, const uint32_t* rest, uint32_
 // Pixel list (into `out`) of the wave-sized slot groups ordered by the probe costs in
 // ctx->d_cost, costliest group first (ties keep slot order).
 int sort_groups_by_cost(nart_ctx* ctx, uint32_t n, uint32_t* out, hipStream_t st);
+
+// Sample-major bucket layout: slot `base + p` of a bucket of `cnt` traced pixels keeps sample s
+// at base*spp + s*cnt + p.  One block per bucket of the batch.
+__global__ void k_slot_table(const uint32_t* bucket_base, uint32_t nbk, uint32_t nslots, uint32_t spp, uint2* so) {
+    const uint32_t b = blockIdx.x;
+    const uint32_t base = bucket_base[b], end = b + 1 < nbk ? bucket_base[b + 1] : nslots;
+    for (uint32_t p = threadIdx.x; base + p < end; p += blockDim.x) so[base + p] = make_uint2(base * spp + p, end - base);
+}
+
+__global__ void k_slot_rows(uint32_t n, uint32_t spp, uint2* so) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) so[i] = make_uint2(i * spp, 1u);
+}
 
 __global__ void k_iota(uint32_t* v, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -660,11 +677,58 @@ int dispatch_render(nart_ctx* ctx, const RenderArgs& a, int integrator, hipStrea
     return ctx->variant == 1 ? dispatch_wavefront(ctx, a, st) : dispatch_megakernel(ctx, a, st);
 }
 
-// LatinSquare per traced pixel: LDS variant up to 256 spp, global-memory variant beyond.
+// Filter index of AddSample (render.cpp:43-49) as a function of d2 = distX^2 + distY^2:
+// fi(d2) = min(63, uint8(RN(RN(sqrt(d2)) / fw) * 64)).  sqrt and / are correctly rounded and the
+// scaling by 64 is exact, so below the uint8 wrap fi is a non-decreasing step function of d2 and
+// fi(d2) >= k  <=>  d2 >= thr[k].  thr[0] = 0, thr[64] = inf; thr[k] is found by bisection over the
+// float bit patterns with the same float operations.  A splat hit has |distX|, |distY| <= fw + 0.5,
+// so the thresholds are exact for every hit when RN(sqrt(2) (fw + 0.5) / fw) * 64 stays below 256
+// (fw > ~0.28); otherwise returns false and the splat keeps the direct computation.
+static uint32_t filter_index_host(float d2, float fw) {
+    volatile float dist = std::sqrt(d2);
+    volatile float q = dist / fw;
+    return std::min(63u, (uint32_t)(int32_t)(q * 64.f) & 0xFFu);
+}
+
+bool splat_thresholds(float fw, float thr[65]) {
+    if (!(fw > 0.f)) return false;
+    const float hmax = fw + 0.5f;
+    const double worst = std::sqrt(2.0 * (double)hmax * hmax) / fw * 64.0;
+    if (!(worst < 250.0)) return false;
+    const float d2max = 2.f * hmax * hmax * 1.001f;
+    uint32_t hi_bits;
+    std::memcpy(&hi_bits, &d2max, 4);
+    thr[0] = 0.f;
+    thr[64] = __builtin_inff();
+    for (uint32_t k = 1; k < 64; ++k) {
+        uint32_t lo = 0, hi = hi_bits;  // f(lo) < k <= f(hi) unless no hit reaches index k
+        if (filter_index_host(d2max, fw) < k) {
+            thr[k] = __builtin_inff();
+            continue;
+        }
+        while (hi - lo > 1) {
+            const uint32_t mid = lo + (hi - lo) / 2;
+            float m;
+            std::memcpy(&m, &mid, 4);
+            if (filter_index_host(m, fw) >= k) hi = mid;
+            else lo = mid;
+        }
+        std::memcpy(&thr[k], &hi, 4);
+        if (filter_index_host(0.f, fw) >= k) thr[k] = 0.f;
+    }
+    return true;
+}
+
+// LatinSquare per traced pixel: float arrays in LDS up to 256 spp, LDS index shuffles up to 1024
+// spp (scratch in Lout: 2*spp floats per lane of every launched block, within Lout's 4*spp per
+// slot once there are >= 64 slots), the global-memory variant beyond.
 int launch_latin(nart_ctx* ctx, const RenderArgs& ra, hipStream_t st) {
     if (ra.spp <= 256) {
         size_t lds = (size_t)ra.spp * 2 * 64 * sizeof(float);
         hipLaunchKernelGGL(k_latin_lds, dim3((ra.n_slots + 63) / 64), dim3(64), lds, st, ra);
+    } else if (ra.spp <= 1024 && ra.n_slots >= 64) {
+        size_t lds = (size_t)ra.spp * (ra.spp <= 512 ? 2 : 1) * 64 * sizeof(uint16_t);
+        hipLaunchKernelGGL(k_latin_idx, dim3((ra.n_slots + 63) / 64), dim3(64), lds, st, ra, (float*)ra.Lout);
     } else {
         hipLaunchKernelGGL(k_latin, dim3((ra.n_slots + 255) / 256), dim3(256), 0, st, ra);
     }
@@ -683,10 +747,12 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
     const uint32_t nb_total = g.n_buckets_x * g.n_buckets_y;
     for (uint32_t i = 0; i < n; ++i)
         if (ids[i] >= nb_total) return fail(ctx, NART_E_INVALID, "bucket id out of range");
-    float table[64];
+    // filter table [64] + filter-index thresholds [65] (splat_thresholds)
+    float table[64 + 65];
     nart_filter_table(table);
-    if (!ctx->d_table) HIPCHK(hipMalloc(&ctx->d_table, 64 * sizeof(float)));
-    HIPCHK(hipMemcpyAsync(ctx->d_table, table, sizeof(table), hipMemcpyHostToDevice, st));
+    const bool thr_ok = splat_thresholds(p->filter_width, table + 64);
+    if (!ctx->d_table) HIPCHK(hipMalloc(&ctx->d_table, sizeof(table)));
+    HIPCHK(hipMemcpy(ctx->d_table, table, sizeof(table), hipMemcpyHostToDevice));
 #ifdef NART_WAVEPROF
     const size_t n_cnt = 24 + 8 * 70000 + 4200000;  // + per-wave and per-slot records (development profile)
 #else
@@ -733,8 +799,11 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         HIPCHK(hipMemcpyAsync(ctx->d_slot_xy, xy.data(), (size_t)nslots * 4, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(ctx->d_bucket_ids, ids + b0, (size_t)nbk * 4, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(ctx->d_bucket_base, base.data(), (size_t)nbk * 4, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_slot_table, dim3(nbk), dim3(256), 0, st, ctx->d_bucket_base, nbk, nslots, p->spp,
+                           ctx->d_slot_so);
         RenderArgs ra;
         ra.slot_xy = ctx->d_slot_xy;
+        ra.slot_so = ctx->d_slot_so;
         ra.samples = ctx->d_samples;
         ra.rng0 = ctx->d_rng;
         ra.Lout = ctx->d_L;
@@ -748,7 +817,6 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         ra.lds_nodes = 0;
         ra.gamma = p->roughening_factor * p->roughening_factor;
         ra.counters = ctx->d_counters;
-        ra.sstride = p->spp;
         HIPCHK(hipEventRecord(ctx->ev[3], st));
         rc = launch_latin(ctx, ra, st);
         if (rc) return rc;
@@ -763,6 +831,8 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         sa.Lout = ctx->d_L;
         sa.tiles = d_tiles + (size_t)b0 * tpx * 5;
         sa.table = ctx->d_table;
+        sa.thr = thr_ok ? ctx->d_table + 64 : nullptr;
+        sa.idx_scale = 64.f / p->filter_width;
         sa.n_buckets = nbk;
         sa.spp = p->spp;
         sa.B = p->bucket_size;
@@ -779,7 +849,10 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
             sa.invFw = (m == 0.5f) ? 1.f / p->filter_width : 0.f;
         }
         uint64_t nthreads = (uint64_t)nbk * tpx;
-        hipLaunchKernelGGL(k_splat, dim3((uint32_t)((nthreads + 255) / 256)), dim3(256), 0, st, sa);
+        static const size_t splat_lds =
+            std::getenv("NART_SPLAT_LDS") ? std::strtoull(std::getenv("NART_SPLAT_LDS"), nullptr, 10) : 0;
+        if (sa.thr) hipLaunchKernelGGL(k_splat<true>, dim3((uint32_t)((nthreads + 255) / 256)), dim3(256), splat_lds, st, sa);
+        else hipLaunchKernelGGL(k_splat<false>, dim3((uint32_t)((nthreads + 255) / 256)), dim3(256), splat_lds, st, sa);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(ctx->ev[2], st));
         HIPCHK(hipEventSynchronize(ctx->ev[2]));
@@ -881,6 +954,12 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     if (hipFuncSetAttribute((const void*)k_latin_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
         hipSuccess)
         return bail(NART_E_HIP);
+    if (hipFuncSetAttribute((const void*)k_latin_idx, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+        hipSuccess)
+        return bail(NART_E_HIP);
+    hipFuncSetAttribute((const void*)k_splat<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
+    hipFuncSetAttribute((const void*)k_splat<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
+    (void)hipGetLastError();  // the splat LDS limit is a tuning knob (NART_SPLAT_LDS), not required
     // reference octree visibility (Q14) + device BVH
     std::vector<uint8_t> mask;
     bool root_leaf = false;
@@ -1008,7 +1087,7 @@ void nart_hip_destroy(nart_ctx* ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
     void* bufs[] = {ctx->d_nodes, ctx->d_tri_isect, ctx->d_tris, ctx->d_tri_mesh, ctx->d_meshes, ctx->d_mats,
-                    ctx->d_lights, ctx->d_texs, ctx->d_tex_pool, ctx->d_slot_xy, ctx->d_rng, ctx->d_samples,
+                    ctx->d_lights, ctx->d_texs, ctx->d_tex_pool, ctx->d_slot_xy, ctx->d_slot_so, ctx->d_rng, ctx->d_samples,
                     ctx->d_L, ctx->d_bucket_ids, ctx->d_bucket_base, ctx->d_table, ctx->d_counters, ctx->d_wf, ctx->d_envs, ctx->d_density,
                     ctx->d_oc_nodes, ctx->d_oc_chunks, ctx->d_oc_tris, ctx->d_tri_leaf, ctx->d_oc_lock, ctx->d_oc_heap,
                     ctx->d_queue, ctx->d_cost, ctx->d_keys[0], ctx->d_keys[1], ctx->d_vals[0], ctx->d_vals[1],
@@ -1119,9 +1198,11 @@ int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t
     rc = ensure(ctx, n, p->spp, 1);
     if (rc) return rc;
     HIPCHK(hipMemcpy(ctx->d_slot_xy, xy.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_slot_rows, dim3((n + 255) / 256), dim3(256), 0, 0, n, p->spp, ctx->d_slot_so);
     if (!ctx->d_counters) HIPCHK(hipMalloc(&ctx->d_counters, 24 * sizeof(unsigned long long)));
     RenderArgs ra;
     ra.slot_xy = ctx->d_slot_xy;
+    ra.slot_so = ctx->d_slot_so;
     ra.samples = ctx->d_samples;
     ra.rng0 = ctx->d_rng;
     ra.Lout = ctx->d_L;
@@ -1135,13 +1216,17 @@ int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t
     ra.lds_nodes = 0;
     ra.gamma = p->roughening_factor * p->roughening_factor;
     ra.counters = ctx->d_counters;
-    ra.sstride = p->spp;
     rc = launch_latin(ctx, ra, 0);
     if (rc) return rc;
     rc = dispatch_render(ctx, ra, p->integrator, 0);
     if (rc) return rc;
     HIPCHK(hipMemcpy(out, ctx->d_L, (size_t)n * p->spp * sizeof(float4), hipMemcpyDeviceToHost));
     return NART_OK;
+}
+
+int nart_hip_splat_thresholds(float filter_width, float* thr65) {
+    if (!thr65) return NART_E_INVALID;
+    return splat_thresholds(filter_width, thr65) ? NART_OK : NART_E_INVALID;
 }
 
 int nart_hip_eval_sincos(nart_ctx* ctx, const float* x, uint32_t n, float* s, float* c) {

@@ -47,3 +47,26 @@ def test_hip_create_without_gpu_fails_cleanly(built, glass_scene):
         assert e.code == -3  # NART_E_HIP, no abort
     else:
         raise AssertionError("render context created without a GPU")
+
+
+def test_splat_thresholds_reproduce_filter_index(built):
+    """The splat's filter index from d2 thresholds equals AddSample's
+    uint8((sqrt(d2) / fw) * 64) clamped to 63 (render.cpp:43-49), float32 throughout."""
+    import numpy as np
+    lib = nart_amd.api.hip_lib()
+    rng = np.random.default_rng(7)
+    for fw in (2.0, 1.5, 0.5, 1.0, 3.0, 0.75):
+        thr = np.zeros(65, np.float32)
+        assert lib.nart_hip_splat_thresholds(ctypes.c_float(fw), thr.ctypes.data) == 0
+        hmax = np.float32(fw + 0.5)
+        d2max = np.float32(2) * hmax * hmax
+        d2 = np.concatenate([rng.uniform(0, d2max, 400000).astype(np.float32), thr[1:64],
+                             np.nextafter(thr[1:64], np.float32(0)), np.float32([0.0, d2max])])
+        d2 = d2[np.isfinite(d2) & (d2 <= d2max)]
+        dist = np.sqrt(d2)
+        q = (dist / np.float32(fw)).astype(np.float32) * np.float32(64)
+        want = np.minimum(63, q.astype(np.int32) & 0xFF)
+        got = np.searchsorted(thr[1:64], d2, side="right")  # #{k in 1..63: d2 >= thr[k]}
+        assert np.array_equal(got, want), fw
+    thr = np.zeros(65, np.float32)
+    assert lib.nart_hip_splat_thresholds(ctypes.c_float(0.1), thr.ctypes.data) != 0

@@ -277,3 +277,25 @@ def test_octree_missed_camera_hit_samples(gpu, cornell_scene):
     rs = oracle.Oracle(cornell_scene).render_samples(p, 328, 232, 8, 8)
     assert rs[3, 3, 30, 3] == 0.0
     assert _bits_equal(gs, rs), _report(gs, rs)
+
+
+@pytest.mark.parametrize("spp", [320, 512, 1024, 1040])
+def test_latin_square_high_spp(gpu, glass_scene, glass_oracle, spp):
+    """LatinSquare beyond the 256-spp LDS kernel: index shuffles in LDS with both arrays (<= 512
+    spp) or one array per pass (<= 1024), and the global-memory kernel above that.  Per-sample
+    Li_alpha of an 8x8 block (64 slots: the LDS-index kernel's minimum) and a 7x5 block (global
+    kernel), bounces 1 so the samples' camera rays carry the Latin-square positions."""
+    r = nart_amd.HipRenderer(glass_scene)
+    p = _params(glass_scene, 64, 64, spp, bounces=1)
+    for x0, y0, w, h in ((20, 20, 8, 8), (3, 50, 7, 5)):
+        g = r.render_samples(p, x0, y0, w, h)
+        o = glass_oracle.render_samples(p, x0, y0, w, h)
+        assert _bits_equal(g, o), _report(g, o)
+
+
+def test_latin_square_high_spp_frame(gpu, glass_scene, glass_oracle):
+    """Bucket layout at 512 spp (LDS-index LatinSquare, sample-major buckets, splat): framebuffer."""
+    p = _params(glass_scene, 24, 20, 512, bounces=2)
+    g = nart_amd.HipRenderer(glass_scene).render(p)
+    o = glass_oracle.render(p)
+    assert _bits_equal(g, o), _report(g, o)
