@@ -235,4 +235,128 @@ __global__ __launch_bounds__(256) void k_render_volume(DScene S, RenderArgs A) {
     if (COUNT) atomicAdd(&A.counters[0], (unsigned long long)A.spp);
 }
 
+// The same computation as a per-lane state machine (the default).  k_render_volume runs li_volume
+// to completion for every sample, so a wave waits for its slowest lane at every sample and costs
+// sum_s max_lane(collisions); the number of collisions per sample is roughly geometric, so that is
+// several times the mean.  Here one loop iteration advances every lane by one tentative collision
+// (plus whatever cheap steps lead up to it: a new sample, a new ray segment, the next majorant
+// segment), and a lane whose sample ends starts its next sample at once, so the wave costs about
+// max_lane sum_s(collisions).  Each lane performs exactly the RNG draws and float operations of
+// li_volume in the same order: the output is bit-identical.
+template <bool COUNT>
+__global__ __launch_bounds__(256) void k_render_volume_sm(DScene S, RenderArgs A) {
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= A.n_slots) return;
+    const uint32_t slot = A.queue ? A.queue[gid] : gid;
+    const uint32_t xy = A.slot_xy[slot];
+    const uint32_t px = xy & 0xFFFFu, py = xy >> 16;
+    uint32_t rng = A.rng0[slot];
+    const uint2 so = A.slot_so[slot];
+    const float2* smp = A.samples + so.x;
+    float4* out = A.Lout + so.x;
+    const DMedium& m = S.medium;
+    const f3 beta = F3(1.f, 1.f, 1.f);
+    enum { P_SAMPLE, P_RAY, P_MAJ, P_COLL, P_ESC };
+    uint32_t work = 0, s = 0, bounce = 0;
+    int ph = P_SAMPLE;
+    f3 o = F3(0.f, 0.f, 0.f), d = o, ro = o, rd = o, L = o;
+    float uMode = 0.f, sigma = 1.f, tMin = 0.f, t1 = 0.f;
+    MajIter it;
+    for (;;) {
+        bool finish = false;
+        if (ph == P_SAMPLE) {
+            if (s >= A.spp) break;
+            const float2 sm = smp[s * so.y];
+            const Ray r = cast_ray(S, F2(sm.x, sm.y), A.W, A.H, px, py);
+            o = r.o;
+            d = r.d;
+            L = F3(0.f, 0.f, 0.f);
+            bounce = 0;
+            ph = P_RAY;
+        }
+        if (ph == P_RAY) {  // top of VolumeIntegrator's bounce loop
+            (void)rng_float(rng);  // u: passed to SampleT_maj, unused there
+            uMode = rng_float(rng);
+            if (m.present && medium_sample_ray(m, o, d, it)) {
+                ro = o;
+                rd = d;
+                ph = P_MAJ;
+            } else {
+                ph = P_ESC;
+            }
+        }
+        if (ph == P_MAJ) {
+            float t0;
+            if (maj_next(m, it, sigma, t0, t1)) {
+                tMin = t0;
+                ph = P_COLL;
+            } else {
+                ph = P_ESC;
+            }
+        }
+        if (ph == P_COLL) {
+            ++work;
+            const float t = tMin + (-glibc_logf(1.f - rng_float(rng)) / sigma);
+            if (!(t < t1)) {
+                ph = P_MAJ;
+            } else {
+                const f3 p = add(ro, muls(rd, t));
+                if (p.x < m.bmin[0] || p.y < m.bmin[1] || p.z < m.bmin[2] || p.x > m.bmax[0] || p.y > m.bmax[1] ||
+                    p.z > m.bmax[2]) {
+                    ph = P_ESC;
+                } else {
+                    const f3 bmin = F3(m.bmin[0], m.bmin[1], m.bmin[2]);
+                    const f3 bs = sub(F3(m.bmax[0], m.bmax[1], m.bmax[2]), bmin);
+                    const f3 q0 = sub(p, bmin);
+                    const float density = dg_lookup(m, F3(q0.x / bs.x, q0.y / bs.y, q0.z / bs.z));
+                    const float sa = m.sigma_a * density, ss = m.sigma_s * density;
+                    const float pAbsorb = sa / sigma;
+                    const float pScatter = ss / sigma;
+                    if (uMode < pAbsorb) {
+                        L = add(L, mul(muls(F3(m.Le[0], m.Le[1], m.Le[2]), density), beta));
+                        finish = true;
+                    } else if (uMode < pAbsorb + pScatter) {
+                        if (bounce++ > A.bounces) {
+                            finish = true;
+                        } else {
+                            const float a = rng_float(rng);
+                            const float b = rng_float(rng);
+                            o = p;
+                            d = uniform_sample_sphere(F2(a, b));
+                            ph = P_RAY;
+                        }
+                    } else {
+                        uMode = rng_float(rng);  // null collision
+                        tMin = t;
+                    }
+                }
+            }
+        }
+        if (ph == P_ESC) {
+            float lightTMax = __builtin_inff();
+            f3 Le = F3(0.f, 0.f, 0.f);
+            for (uint32_t j = 0; j < S.num_lights; ++j) {
+                float lt = __builtin_inff();
+                const f3 Li = light_li(S, S.lights[j], o, d, nullptr, lt);
+                if (lt < lightTMax) {
+                    Le = Li;
+                    lightTMax = lt;
+                }
+            }
+            L = add(L, mul(Le, beta));
+            finish = true;
+        }
+        if (finish) {
+            out[s * so.y] = make_float4(L.x, L.y, L.z, 1.f);
+            ++s;
+            ph = P_SAMPLE;
+        }
+    }
+    if (A.cost) {
+        A.cost[gid] = work + A.spp;
+        return;
+    }
+    if (COUNT) atomicAdd(&A.counters[0], (unsigned long long)A.spp);
+}
+
 }  // namespace nd

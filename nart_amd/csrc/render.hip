@@ -640,18 +640,20 @@ int dispatch_wavefront(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     return c ? run_wavefront<32, true>(ctx, a, st) : run_wavefront<32, false>(ctx, a, st);
 }
 
-// Volume integrator.  Its lanes run each sample to completion in lock step, so a wave costs
-// the sum over samples of its slowest lane and refilling single lanes would not help; when the
-// shard spans several rounds of resident waves, the costliest wave-sized pixel groups (cost
-// probe: tentative collisions of 4 samples per pixel) are launched first.
+// Volume integrator: k_render_volume_sm (lanes advance one tentative collision per iteration and
+// start their next sample independently).  When the shard spans several rounds of resident
+// waves, the costliest wave-sized pixel groups (cost probe: tentative collisions of 4 samples per
+// pixel) are launched first.
 int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     const dim3 block(256);
     const uint32_t blocks = (a.n_slots + 255) / 256;
+    // NART_VOL_SM=0: the per-sample lock-step kernel (A/B timing only; same output)
+    static const bool sm = !(std::getenv("NART_VOL_SM") && std::getenv("NART_VOL_SM")[0] == '0');
     RenderArgs b = a;
     if (queue_mode() == 2) {
         int cus = 0, per_cu = 0;
         HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_render_volume<false>, 256, 0));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_render_volume_sm<false>, 256, 0));
         const uint32_t resident = (uint32_t)std::max(1, cus * std::max(per_cu, 1));
         const uint32_t n = a.n_slots;
         if (blocks > resident && (double)n / (256.0 * resident) < 12.0 && a.spp > 4) {
@@ -660,14 +662,20 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             RenderArgs pb = a;
             pb.spp = 4;
             pb.cost = ctx->d_cost;
-            hipLaunchKernelGGL((k_render_volume<false>), dim3(blocks), block, 0, st, ctx->scene, pb);
+            if (sm) hipLaunchKernelGGL((k_render_volume_sm<false>), dim3(blocks), block, 0, st, ctx->scene, pb);
+            else hipLaunchKernelGGL((k_render_volume<false>), dim3(blocks), block, 0, st, ctx->scene, pb);
             rc = sort_groups_by_cost(ctx, n, ctx->d_queue, st);
             if (rc) return rc;
             b.queue = ctx->d_queue;
         }
     }
-    if (ctx->counters) hipLaunchKernelGGL((k_render_volume<true>), dim3(blocks), block, 0, st, ctx->scene, b);
-    else hipLaunchKernelGGL((k_render_volume<false>), dim3(blocks), block, 0, st, ctx->scene, b);
+    if (sm) {
+        if (ctx->counters) hipLaunchKernelGGL((k_render_volume_sm<true>), dim3(blocks), block, 0, st, ctx->scene, b);
+        else hipLaunchKernelGGL((k_render_volume_sm<false>), dim3(blocks), block, 0, st, ctx->scene, b);
+    } else {
+        if (ctx->counters) hipLaunchKernelGGL((k_render_volume<true>), dim3(blocks), block, 0, st, ctx->scene, b);
+        else hipLaunchKernelGGL((k_render_volume<false>), dim3(blocks), block, 0, st, ctx->scene, b);
+    }
     HIPCHK(hipGetLastError());
     return NART_OK;
 }
