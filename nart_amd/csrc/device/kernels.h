@@ -270,6 +270,9 @@ enum { ST_EXT = 0, ST_SH1 = 1, ST_SH2 = 2 };
 #define SECT(i, t) ((void)0)
 #endif
 #define NART_RENDER_LB __launch_bounds__(256, NART_RENDER_WAVES)
+#ifndef NART_QUORUM
+#define NART_QUORUM 8  // C3: 0 (lock step per query) 593 ms, 4: 530, 8: 517, 12: 518, 32: 595; -1: traverse() 569
+#endif
 template <int MAXL, bool COUNT, bool ENV>
 __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
     // LDS traversal stack: stack_depth entries of (node code, entry distance) per lane,
@@ -332,8 +335,12 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
     uint64_t sect[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const uint64_t sect_t0 = SECT_T();
 #endif
+    // Query in flight across loop iterations (traversal quorum, below).
+    Trav tq;
+    bool tracing = false;
     for (;;) {
         uint64_t st0 = SECT_T();
+        if (!tracing) {
         if (A.qhead) {
             // refill lanes whose pixel is done: one queue atomic per wave
             const bool need = new_sample && s >= A.spp;
@@ -401,14 +408,38 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
         }
         SECT(1, st0);
         st0 = SECT_T();
+#if NART_QUORUM >= 0
+        trav_begin(S, cur, tmax, stage != ST_EXT, tq);
+        tracing = S.geometry_visible;  // one-chunk scenes render no geometry (Q14)
+#endif
+        }  // !tracing
 
         float bt;
         uint32_t bg;
+#if NART_QUORUM >= 0
+        // Traversal with a quorum: lanes whose query resolves idle until at most NART_QUORUM lanes
+        // of the wave are still tracing; then the resolved lanes shade and set up their next
+        // query while the rest keep their traversal state (tq) for the next iteration.  With 0
+        // every query of the wave resolves first (lock step per query).  Only the interleaving
+        // of lanes changes; each lane's operations are the same.
+        for (;;) {
+            if (tracing && trav_step<COUNT>(S, cur, tq, sc, stn, stride, cnt, s_nodes, nl)) tracing = false;
+            if (__popcll(__ballot(tracing)) <= NART_QUORUM) break;
+        }
+        if (tracing) continue;
+        bt = tq.bestT;
+        bg = tq.bestG;
+        if (S.geometry_visible)
+            oc_resolve<COUNT>(S, cur, tmax, stage != ST_EXT, tq.risky, tq.bestInfo, fminf(tq.t2, oc_cull(S, tq.bestT)),
+                              bt, bg, cnt);
+        const bool hit = bg != NO_HIT;
+#else
 #ifdef NART_WAVEPROF
         const uint64_t prof_t1 = __builtin_amdgcn_s_memtime();
         const uint32_t prof_n0 = cnt.nodes, prof_t0n = cnt.tris;
         ++prof_iters;
 #endif
+        tracing = false;
         const bool hit = traverse<COUNT>(S, cur, tmax, stage != ST_EXT, bt, bg, sc, stn, stride, cnt, s_nodes, nl);
 #ifdef NART_WAVEPROF
         if (COUNT) {
@@ -426,6 +457,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
         }
 #endif
 
+#endif  // NART_QUORUM
         SECT(2, st0);
         st0 = SECT_T();
         bool resolve = false;
