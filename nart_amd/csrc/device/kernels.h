@@ -430,8 +430,8 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
         bt = tq.bestT;
         bg = tq.bestG;
         if (S.geometry_visible)
-            oc_resolve<COUNT>(S, cur, tmax, stage != ST_EXT, tq.risky, tq.bestInfo, fminf(tq.t2, oc_cull(S, tq.bestT)),
-                              bt, bg, cnt);
+            oc_resolve<COUNT>(S, cur, tq.tmax, tq.any, tq.risky, tq.bestInfo, fminf(tq.t2, oc_cull(S, tq.bestT)), bt,
+                              bg, cnt);
         const bool hit = bg != NO_HIT;
 #else
 #ifdef NART_WAVEPROF
@@ -727,15 +727,49 @@ ND bool splat_hits_thr(const SplatArgs& A, const float* table, const float* thr,
     return hit;
 }
 
-template <bool THR>
+// Per-lane constants of splat_hits_fast: the tile pixel in image coordinates for a sample of the
+// lane's own bucket column / row (xsA, ysA) and of the next one (xsB, ysB), and the coordinate
+// from which a sample counts as the next bucket's (edge = bucket origin + B + fb).
+struct SplatLane {
+    float xsA, xsB, ysA, ysB, edgeX, edgeY;
+};
+
+// splat_hits_thr for a power-of-two bucket size, with the per-pair work cut to compares:
+//  * k = floor((sc - fb) / B): sc - fb is exact (both are multiples of ulp(sc)) and lies in
+//    [origin + S, origin + S + 1] for bucket-local column S, and / B is exact, so k is the bucket
+//    column, plus one exactly when sc - fb >= origin + B, i.e. sc >= edge;
+//  * floor(a) <= xs  <=>  a < xs + 1  and  xs < ceil(b)  <=>  xs < b  for an integer xs, with
+//    a = RN(sc - fw) and b = RN(sc + fw) as the reference rounds them;
+//  * dist and the filter index as in splat_hits_thr.
+ND bool splat_hits_fast(const SplatArgs& A, const SplatLane& P, const float* table, const float* thr, float scx,
+                        float scy, float& w) {
+    const float xs = scx >= P.edgeX ? P.xsB : P.xsA;
+    const float ys = scy >= P.edgeY ? P.ysB : P.ysA;
+    const bool hit = (scx - A.fw) < xs + 1.f && xs < (scx + A.fw) && (scy - A.fw) < ys + 1.f && ys < (scy + A.fw);
+    const float distX = (xs + 0.5f) - scx;
+    const float distY = (ys + 0.5f) - scy;
+    const float d2 = distX * distX + distY * distY;
+    int g = (int)(__builtin_amdgcn_sqrtf(d2) * A.idx_scale);
+    g = g < 0 ? 0 : (g > 63 ? 63 : g);
+    const float t0 = thr[g], t1 = thr[g + 1];
+    const int fi = g - (d2 < t0 ? 1 : 0) + (d2 >= t1 ? 1 : 0);
+    w = table[fi];
+    return hit;
+}
+
+// MODE 0: direct AddSample arithmetic (splat_hits); 1: filter index from thresholds
+// (splat_hits_thr); 2: thresholds and a power-of-two bucket size (splat_hits_fast).
+template <int MODE>
 __global__ __launch_bounds__(256) void k_splat(SplatArgs A) {
     __shared__ float s_table[64];
     __shared__ float s_thr[65];
     if (threadIdx.x < 64) s_table[threadIdx.x] = A.table[threadIdx.x];
-    if (THR && threadIdx.x < 65) s_thr[threadIdx.x] = A.thr[threadIdx.x];
+    if (MODE > 0 && threadIdx.x < 65) s_thr[threadIdx.x] = A.thr[threadIdx.x];
     __syncthreads();
-#define NART_SPLAT_HITS(scx, scy, w) \
-    (THR ? splat_hits_thr(A, s_table, s_thr, scx, scy, tx, ty, w) : splat_hits(A, s_table, scx, scy, tx, ty, w))
+#define NART_SPLAT_HITS(scx, scy, w)                                                                        \
+    (MODE == 2   ? splat_hits_fast(A, P, s_table, s_thr, scx, scy, w)                                      \
+     : MODE == 1 ? splat_hits_thr(A, s_table, s_thr, scx, scy, tx, ty, w)                                  \
+                 : splat_hits(A, s_table, scx, scy, tx, ty, w))
     const uint32_t tpx = A.tile * A.tile;
     const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (uint64_t)A.n_buckets * tpx) return;
@@ -748,6 +782,13 @@ __global__ __launch_bounds__(256) void k_splat(SplatArgs A) {
     const int bw = (int)(x1 - x0), bh = (int)(y1 - y0);
     const uint32_t npx = (uint32_t)(bw * bh);
     const uint32_t base = A.bucket_base[bi];
+    SplatLane P;
+    P.xsA = (float)(tx + x0);
+    P.xsB = (float)(tx + x0 + A.B);
+    P.ysA = (float)(ty + y0);
+    P.ysB = (float)(ty + y0 + A.B);
+    P.edgeX = (float)(x0 + A.B + A.fb);
+    P.edgeY = (float)(y0 + A.B + A.fb);
     // Candidate source pixels.  A sample of bucket-local column S has sc - x0 in [S+fb, S+fb+1],
     // so its splat columns span [S+fb-ceil(fw), S+fb+1+fw): tile column tx can only be reached
     // from S in [tx-fb-ceil(fw), tx-fb+ceil(fw)].  Samples of the last column can also wrap to

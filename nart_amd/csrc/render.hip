@@ -859,8 +859,11 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         uint64_t nthreads = (uint64_t)nbk * tpx;
         static const size_t splat_lds =
             std::getenv("NART_SPLAT_LDS") ? std::strtoull(std::getenv("NART_SPLAT_LDS"), nullptr, 10) : 0;
-        if (sa.thr) hipLaunchKernelGGL(k_splat<true>, dim3((uint32_t)((nthreads + 255) / 256)), dim3(256), splat_lds, st, sa);
-        else hipLaunchKernelGGL(k_splat<false>, dim3((uint32_t)((nthreads + 255) / 256)), dim3(256), splat_lds, st, sa);
+        static const int splat_mode = std::getenv("NART_SPLAT_MODE") ? std::atoi(std::getenv("NART_SPLAT_MODE")) : 2;
+        const dim3 sg((uint32_t)((nthreads + 255) / 256));
+        if (sa.thr && sa.invB != 0.f && splat_mode >= 2) hipLaunchKernelGGL(k_splat<2>, sg, dim3(256), splat_lds, st, sa);
+        else if (sa.thr && splat_mode >= 1) hipLaunchKernelGGL(k_splat<1>, sg, dim3(256), splat_lds, st, sa);
+        else hipLaunchKernelGGL(k_splat<0>, sg, dim3(256), splat_lds, st, sa);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(ctx->ev[2], st));
         HIPCHK(hipEventSynchronize(ctx->ev[2]));
@@ -965,8 +968,9 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     if (hipFuncSetAttribute((const void*)k_latin_idx, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
         hipSuccess)
         return bail(NART_E_HIP);
-    hipFuncSetAttribute((const void*)k_splat<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
-    hipFuncSetAttribute((const void*)k_splat<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
+    hipFuncSetAttribute((const void*)k_splat<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
+    hipFuncSetAttribute((const void*)k_splat<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
+    hipFuncSetAttribute((const void*)k_splat<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
     (void)hipGetLastError();  // the splat LDS limit is a tuning knob (NART_SPLAT_LDS), not required
     // reference octree visibility (Q14) + device BVH
     std::vector<uint8_t> mask;
