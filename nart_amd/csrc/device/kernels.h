@@ -273,8 +273,14 @@ enum { ST_EXT = 0, ST_SH1 = 1, ST_SH2 = 2 };
 #ifndef NART_QUORUM
 #define NART_QUORUM 8  // C3: 0 (lock step per query) 593 ms, 4: 530, 8: 517, 12: 518, 32: 595; -1: traverse() 569
 #endif
+#ifndef NART_QUORUM_ENV
+// environment-light scenes (more shading registers and work per hit): C4 1/8 shard -1: 645 ms,
+// 0: 668, 8: 701
+#define NART_QUORUM_ENV -1
+#endif
 template <int MAXL, bool COUNT, bool ENV>
 __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
+    constexpr int QUORUM = ENV ? NART_QUORUM_ENV : NART_QUORUM;
     // LDS traversal stack: stack_depth entries of (node code, entry distance) per lane,
     // laid out [depth][lane] so a wave's 64 lanes hit 64 distinct banks.
     extern __shared__ __attribute__((aligned(16))) int s_dyn[];
@@ -408,23 +414,24 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
         }
         SECT(1, st0);
         st0 = SECT_T();
-#if NART_QUORUM >= 0
-        trav_begin(S, cur, tmax, stage != ST_EXT, tq);
-        tracing = S.geometry_visible;  // one-chunk scenes render no geometry (Q14)
-#endif
+        if constexpr (QUORUM >= 0) {
+            trav_begin(S, cur, tmax, stage != ST_EXT, tq);
+            tracing = S.geometry_visible;  // one-chunk scenes render no geometry (Q14)
+        }
         }  // !tracing
 
         float bt;
         uint32_t bg;
-#if NART_QUORUM >= 0
-        // Traversal with a quorum: lanes whose query resolves idle until at most NART_QUORUM lanes
+        bool hit;
+        if constexpr (QUORUM >= 0) {
+        // Traversal with a quorum: lanes whose query resolves idle until at most QUORUM lanes
         // of the wave are still tracing; then the resolved lanes shade and set up their next
         // query while the rest keep their traversal state (tq) for the next iteration.  With 0
         // every query of the wave resolves first (lock step per query).  Only the interleaving
         // of lanes changes; each lane's operations are the same.
         for (;;) {
             if (tracing && trav_step<COUNT>(S, cur, tq, sc, stn, stride, cnt, s_nodes, nl)) tracing = false;
-            if (__popcll(__ballot(tracing)) <= NART_QUORUM) break;
+            if (__popcll(__ballot(tracing)) <= QUORUM) break;
         }
         if (tracing) continue;
         bt = tq.bestT;
@@ -432,15 +439,15 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
         if (S.geometry_visible)
             oc_resolve<COUNT>(S, cur, tq.tmax, tq.any, tq.risky, tq.bestInfo, fminf(tq.t2, oc_cull(S, tq.bestT)), bt,
                               bg, cnt);
-        const bool hit = bg != NO_HIT;
-#else
+        hit = bg != NO_HIT;
+        } else {
 #ifdef NART_WAVEPROF
         const uint64_t prof_t1 = __builtin_amdgcn_s_memtime();
         const uint32_t prof_n0 = cnt.nodes, prof_t0n = cnt.tris;
         ++prof_iters;
 #endif
         tracing = false;
-        const bool hit = traverse<COUNT>(S, cur, tmax, stage != ST_EXT, bt, bg, sc, stn, stride, cnt, s_nodes, nl);
+        hit = traverse<COUNT>(S, cur, tmax, stage != ST_EXT, bt, bg, sc, stn, stride, cnt, s_nodes, nl);
 #ifdef NART_WAVEPROF
         if (COUNT) {
             const uint32_t dn = cnt.nodes - prof_n0;
@@ -456,8 +463,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
             if (stage == ST_EXT && hit) WPROF(cnt, 8);
         }
 #endif
-
-#endif  // NART_QUORUM
+        }  // QUORUM
         SECT(2, st0);
         st0 = SECT_T();
         bool resolve = false;
