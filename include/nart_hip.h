@@ -84,7 +84,9 @@ int nart_hip_eval_sincos(nart_ctx* ctx, const float* x, uint32_t n, float* sin_o
    them (the splat then evaluates sqrt and division per pair). */
 int nart_hip_splat_thresholds(float filter_width, float* thr65);
 
-/* Kernel variant: 0 = megakernel (one lane per pixel slot), 1 = wavefront (ray queues). */
+/* Kernel variant: 0 = megakernel (one lane per pixel slot; traversal quorum on when the launch
+   spans >= 3 rounds of resident waves), 1 = wavefront (ray queues), 2 = megakernel with the
+   traversal quorum on for every launch (parity tests of that path at small sizes). */
 int nart_hip_set_variant(nart_ctx* ctx, int variant);
 
 #ifdef __cplusplus

@@ -278,9 +278,11 @@ enum { ST_EXT = 0, ST_SH1 = 1, ST_SH2 = 2 };
 // 0: 668, 8: 701
 #define NART_QUORUM_ENV -1
 #endif
-template <int MAXL, bool COUNT, bool ENV>
+// QR: traversal quorum on (throughput-bound launches: many rounds of resident waves) or off
+// (small shards, whose costliest pixels' serial chains set the time: the quorum lengthens them).
+template <int MAXL, bool COUNT, bool ENV, bool QR>
 __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
-    constexpr int QUORUM = ENV ? NART_QUORUM_ENV : NART_QUORUM;
+    constexpr int QUORUM = QR ? (ENV ? NART_QUORUM_ENV : NART_QUORUM) : -1;
     // LDS traversal stack: stack_depth entries of (node code, entry distance) per lane,
     // laid out [depth][lane] so a wave's 64 lanes hit 64 distinct banks.
     extern __shared__ __attribute__((aligned(16))) int s_dyn[];

@@ -442,34 +442,40 @@ int sort_groups_by_cost(nart_ctx* ctx, uint32_t n, uint32_t* out, hipStream_t st
 
 template <int MAXL, bool COUNT, bool ENV>
 int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
-    auto kern = k_render<MAXL, COUNT, ENV>;
+    auto kern = k_render<MAXL, COUNT, ENV, false>;
+    auto kern_q = k_render<MAXL, COUNT, ENV, true>;
     static bool attr = false;  // dynamic LDS above the 64 KiB default
     if (!attr) {
-        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        hipFuncSetAttribute((const void*)k_render<MAXL, true, ENV>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024);
+        for (const void* f : {(const void*)kern, (const void*)kern_q, (const void*)k_render<MAXL, true, ENV, false>})
+            hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
+    // NART_QUORUM_MIN_ROUNDS: rounds of resident waves from which the quorum kernel is used (C3:
+    // whole frame 16 rounds 569 -> 517 ms with it, 1/2 frame 8 rounds 332 -> 301, 1/4 4 rounds
+    // 183 -> 179, 1/8 2 rounds 108 -> 134)
+    static const double q_rounds =
+        std::getenv("NART_QUORUM_MIN_ROUNDS") ? std::atof(std::getenv("NART_QUORUM_MIN_ROUNDS")) : 3.0;
     RenderArgs b = a;
     b.lds_nodes = render_lds_nodes(ctx);
     const size_t lds = (size_t)ctx->stack_depth * 256 * 8 + (size_t)b.lds_nodes * sizeof(BVHNode);
     const dim3 block(256);
     uint32_t blocks = (a.n_slots + 255) / 256;
     const int mode = queue_mode();
+    int cus = 0, per_cu = 0;
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 256, lds));
+    const uint32_t resident = (uint32_t)std::max(1, cus * std::max(per_cu, 1));
+    const uint32_t W = resident * 4;  // resident (persistent) waves
+    const double R = (double)a.n_slots / (64.0 * W);  // rounds of resident waves
+    if (ctx->variant == 2 || R >= q_rounds) kern = kern_q;
     if (mode > 0) {
-        int cus = 0, per_cu = 0;
-        HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 256, lds));
-        const uint32_t resident = (uint32_t)std::max(1, cus * std::max(per_cu, 1));
         if (blocks > resident) {  // more pixels than resident lanes: persistent grid + queue
             const uint32_t n = a.n_slots;
             int rc = ensure_queue(ctx, n);
             if (rc) return rc;
             const dim3 eg((n + 255) / 256);
-            const uint32_t W = resident * 4;  // persistent waves
             // costly pixels per first-round wave: few when the shard is small (their serial chains
             // bound the frame), all 64 (packed, launched first) when there are many rounds
-            const double R = (double)n / (64.0 * W);
             uint32_t k = R >= 3.0 ? 32u : 8u;  // measured on C3 shards of 1/2, 1/4, 1/8 of the frame
             if (R >= 12.0 && mode == 2 && !std::getenv("NART_QUEUE_K")) {
                 // many rounds: the slot order (costly waves interleaved with cheap ones in time)
@@ -486,7 +492,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                 RenderArgs pb = b;  // cost probe: the first sample of every pixel
                 pb.spp = 1;
                 pb.cost = ctx->d_cost;
-                hipLaunchKernelGGL((k_render<MAXL, true, ENV>), dim3(blocks), block, lds, st, ctx->scene, pb);
+                hipLaunchKernelGGL((k_render<MAXL, true, ENV, false>), dim3(blocks), block, lds, st, ctx->scene, pb);
                 int rc2 = sort_groups_by_cost(ctx, n, k == 64u ? ctx->d_queue : ctx->d_cost, st);
                 if (rc2) return rc2;
                 size_t tmp = 0;
@@ -949,7 +955,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     if (!ctx) return NART_E_OOM;
     *out = nullptr;
     ctx->device = device_id;
-    if (const char* v = std::getenv("NART_VARIANT")) ctx->variant = std::atoi(v) == 1 ? 1 : 0;
+    if (const char* v = std::getenv("NART_VARIANT")) ctx->variant = std::max(0, std::min(2, std::atoi(v)));
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device_id || device_id < 0) {
         delete ctx;
@@ -1126,8 +1132,8 @@ int nart_hip_set_counters(nart_ctx* ctx, int enable) {
 
 int nart_hip_set_variant(nart_ctx* ctx, int variant) {
     if (!ctx) return NART_E_INVALID;
-    if (variant != 0 && variant != 1)
-        return fail(ctx, NART_E_UNSUPPORTED, "variant must be 0 (megakernel) or 1 (wavefront)");
+    if (variant < 0 || variant > 2)
+        return fail(ctx, NART_E_UNSUPPORTED, "variant must be 0 (megakernel), 1 (wavefront) or 2 (megakernel, quorum always)");
     ctx->variant = variant;
     return NART_OK;
 }

@@ -31,10 +31,10 @@ def _report(a, b):
     return "%d of %d floats differ, max abs diff %g" % (int(ne.sum()), ne.size, float(np.nanmax(np.abs(a - b))))
 
 
-VARIANTS = [0, 1]  # megakernel, wavefront
+VARIANTS = [0, 1, 2]  # megakernel, wavefront, megakernel with the traversal quorum forced on
 
 
-@pytest.fixture(scope="module", params=VARIANTS, ids=["megakernel", "wavefront"])
+@pytest.fixture(scope="module", params=VARIANTS, ids=["megakernel", "wavefront", "quorum"])
 def glass_gpu(request, gpu, glass_scene):
     return nart_amd.HipRenderer(glass_scene, variant=request.param)
 
@@ -251,7 +251,7 @@ def test_bucket_api_matches_render(gpu, glass_gpu, glass_scene):
 C2_OCTREE_BUCKETS = [1356, 1403, 1476, 1700, 1820, 2676, 3203, 4020, 4121, 5083, 5196, 6922, 7286, 7820, 8106]
 
 
-@pytest.mark.parametrize("variant", VARIANTS, ids=["megakernel", "wavefront"])
+@pytest.mark.parametrize("variant", VARIANTS, ids=["megakernel", "wavefront", "quorum"])
 def test_octree_boundary_rejections(gpu, cornell_scene, variant):
     import torch
     p = _params(cornell_scene, 1920, 1080, 64)
