@@ -880,6 +880,153 @@ __global__ __launch_bounds__(256) void k_splat(SplatArgs A) {
     o[4] = ws;
 }
 
+// Four vertically adjacent tile pixels per lane (power-of-two buckets, threshold filter index:
+// the splat_hits_fast arithmetic).  Consecutive lanes take consecutive tile columns, so a wave's
+// loads of sample i cover contiguous source pixels as in k_splat, and each loaded sample serves
+// up to four pixels (8 source rows x 5 columns per 4 pixels instead of 4 x 25: the splat is
+// bound by re-fetching samples through a 4 %-hit L2).  The four pixels share their candidate
+// columns; their candidate rows are windows of one union range (plus the bucket-edge wrap row),
+// visited in ascending order, so each pixel still receives its samples in the reference's
+// (source pixel raster, sample) order.  Per-sample work (position, bucket-edge tests, the
+// column test and x distance) is shared.  (Four horizontal pixels per lane measured slower:
+// lanes then read source pixels four apart and the L1 misses rose by a third.)
+__global__ __launch_bounds__(256) void k_splat_col4(SplatArgs A) {
+    __shared__ float s_table[64];
+    __shared__ float s_thr[65];
+    if (threadIdx.x < 64) s_table[threadIdx.x] = A.table[threadIdx.x];
+    if (threadIdx.x < 65) s_thr[threadIdx.x] = A.thr[threadIdx.x];
+    __syncthreads();
+    const uint32_t gpc = (A.tile + 3) / 4, lpb = A.tile * gpc;  // lane groups per tile column / bucket
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (uint64_t)A.n_buckets * lpb) return;
+    const uint32_t bi = (uint32_t)(gid / lpb), rem = (uint32_t)(gid % lpb);
+    const uint32_t tx = rem % A.tile, ty0 = (rem / A.tile) * 4;
+    const uint32_t bid = A.bucket_ids[bi];
+    const uint32_t bx = bid % A.nbx, by = bid / A.nbx;
+    const uint32_t x0 = A.B * bx, y0 = A.B * by;
+    const uint32_t x1 = min(A.B * (bx + 1), A.totalW), y1 = min(A.B * (by + 1), A.totalH);
+    const int bw = (int)(x1 - x0), bh = (int)(y1 - y0);
+    const uint32_t npx = (uint32_t)(bw * bh);
+    const uint32_t base = A.bucket_base[bi];
+    const int r = (int)ceilf(A.fw), fb = (int)A.fb;
+    const int sxlo = max(0, (int)tx - fb - r), sxhi = min(bw - 1, (int)tx - fb + r);
+    const bool wrapx = bw == (int)A.B && (int)tx <= fb + r + 1 && bw - 1 > sxhi;
+    const int ncol = (sxhi >= sxlo ? sxhi - sxlo + 1 : 0) + (wrapx ? 1 : 0);
+    int lo[4], hi[4];
+    bool val[4], wr[4];
+    int ulo = 1 << 30, uhi = -1;
+    bool anywrap = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int ty = (int)ty0 + j;
+        val[j] = ty < (int)A.tile;
+        lo[j] = max(0, ty - fb - r);
+        hi[j] = min(bh - 1, ty - fb + r);
+        wr[j] = val[j] && bh == (int)A.B && ty <= fb + r + 1 && bh - 1 > hi[j];
+        if (val[j] && hi[j] >= lo[j]) {
+            ulo = min(ulo, lo[j]);
+            uhi = max(uhi, hi[j]);
+        }
+        anywrap = anywrap || wr[j];
+    }
+    const bool extra = anywrap && bh - 1 > uhi;
+    const int nrow = (uhi >= ulo ? uhi - ulo + 1 : 0) + (extra ? 1 : 0);
+    const float fw = A.fw;
+    const float xsA = (float)(tx + x0), xsB = (float)(tx + x0 + A.B);
+    const float ysA0 = (float)(ty0 + y0), ysB0 = (float)(ty0 + y0 + A.B);
+    const float edgeX = (float)(x0 + A.B + A.fb), edgeY = (float)(y0 + A.B + A.fb);
+    float c[4][5];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) c[j][k] = 0.f;
+    for (int ri = 0; ri < nrow; ++ri) {
+        const int sy = (ulo + ri <= uhi) ? ulo + ri : bh - 1;
+        bool act[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) act[j] = val[j] && ((sy >= lo[j] && sy <= hi[j]) || (wr[j] && sy == bh - 1));
+        const float fy = (float)(y0 + (uint32_t)sy + A.fb);
+        for (int ci = 0; ci < ncol; ++ci) {
+            const int sx = (sxlo + ci <= sxhi) ? sxlo + ci : bw - 1;
+            const float fx = (float)(x0 + (uint32_t)sx + A.fb);
+            const uint64_t first = (uint64_t)base * A.spp + (uint32_t)(sy * bw + sx);
+            const float2* sp = A.samples + first;
+            const float4* lp = A.Lout + first;
+            auto splat1 = [&](float2 uv, float4 L) {
+                const float scx = fx + uv.x, scy = fy + uv.y;
+                const float xs = scx >= edgeX ? xsB : xsA;
+                const bool xhit = (scx - fw) < xs + 1.f && xs < (scx + fw);
+                const float distX = (xs + 0.5f) - scx;
+                const float dx2 = distX * distX;
+                const float yb = scy >= edgeY ? ysB0 : ysA0;
+                const float loy = scy - fw, hiy = scy + fw;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (!act[j]) continue;
+                    const float ys = yb + (float)j;
+                    const bool hit = xhit && loy < ys + 1.f && ys < hiy;
+                    const float distY = (ys + 0.5f) - scy;
+                    const float d2 = dx2 + distY * distY;  // = distX^2 + distY^2 (IEEE + commutes)
+                    int g = (int)(__builtin_amdgcn_sqrtf(d2) * A.idx_scale);
+                    g = g < 0 ? 0 : (g > 63 ? 63 : g);
+                    const float t0 = s_thr[g], t1 = s_thr[g + 1];
+                    const int fi = g - (d2 < t0 ? 1 : 0) + (d2 >= t1 ? 1 : 0);
+                    const float w = s_table[fi];
+                    if (hit) {
+                        c[j][0] += L.x * w;
+                        c[j][1] += L.y * w;
+                        c[j][2] += L.z * w;
+                        c[j][3] += L.w * w;
+                        c[j][4] += w;
+                    }
+                }
+            };
+#ifndef NART_COL4_PF
+#define NART_COL4_PF 4
+#endif
+            constexpr uint32_t PF = NART_COL4_PF;  // samples per group; the next group is in flight
+            uint32_t i = 0;
+            float2 nu[PF];
+            float4 nL[PF];
+            if (A.spp >= PF) {
+#pragma unroll
+                for (uint32_t u = 0; u < PF; ++u) {
+                    nu[u] = sp[(size_t)u * npx];
+                    nL[u] = lp[(size_t)u * npx];
+                }
+            }
+            for (; i + PF <= A.spp; i += PF) {
+                float2 uv[PF];
+                float4 Lv[PF];
+#pragma unroll
+                for (uint32_t u = 0; u < PF; ++u) {
+                    uv[u] = nu[u];
+                    Lv[u] = nL[u];
+                }
+                if (i + 2 * PF <= A.spp) {
+                    const size_t k0 = (size_t)(i + PF) * npx;
+#pragma unroll
+                    for (uint32_t u = 0; u < PF; ++u) {
+                        nu[u] = sp[k0 + (size_t)u * npx];
+                        nL[u] = lp[k0 + (size_t)u * npx];
+                    }
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < PF; ++u) splat1(uv[u], Lv[u]);
+            }
+            for (; i < A.spp; ++i) splat1(sp[(size_t)i * npx], lp[(size_t)i * npx]);
+        }
+    }
+    const uint32_t tpx = A.tile * A.tile;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (!val[j]) continue;
+        float* o = A.tiles + ((uint64_t)bi * tpx + (ty0 + j) * A.tile + tx) * 5;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k] = c[j][k];
+    }
+}
+
 // ---------------------------------------------------------------- combine
 struct CombineArgs {
     const float* tiles;  // [bucket id][tile*tile][5]

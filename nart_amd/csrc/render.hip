@@ -865,9 +865,12 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         uint64_t nthreads = (uint64_t)nbk * tpx;
         static const size_t splat_lds =
             std::getenv("NART_SPLAT_LDS") ? std::strtoull(std::getenv("NART_SPLAT_LDS"), nullptr, 10) : 0;
-        static const int splat_mode = std::getenv("NART_SPLAT_MODE") ? std::atoi(std::getenv("NART_SPLAT_MODE")) : 2;
+        static const int splat_mode = std::getenv("NART_SPLAT_MODE") ? std::atoi(std::getenv("NART_SPLAT_MODE")) : 3;
         const dim3 sg((uint32_t)((nthreads + 255) / 256));
-        if (sa.thr && sa.invB != 0.f && splat_mode >= 2) hipLaunchKernelGGL(k_splat<2>, sg, dim3(256), splat_lds, st, sa);
+        const uint64_t n4 = (uint64_t)nbk * g.tile_size * ((g.tile_size + 3) / 4);
+        if (sa.thr && sa.invB != 0.f && splat_mode >= 3)
+            hipLaunchKernelGGL(k_splat_col4, dim3((uint32_t)((n4 + 255) / 256)), dim3(256), 0, st, sa);
+        else if (sa.thr && sa.invB != 0.f && splat_mode >= 2) hipLaunchKernelGGL(k_splat<2>, sg, dim3(256), splat_lds, st, sa);
         else if (sa.thr && splat_mode >= 1) hipLaunchKernelGGL(k_splat<1>, sg, dim3(256), splat_lds, st, sa);
         else hipLaunchKernelGGL(k_splat<0>, sg, dim3(256), splat_lds, st, sa);
         HIPCHK(hipGetLastError());
