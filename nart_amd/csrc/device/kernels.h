@@ -880,7 +880,7 @@ __global__ __launch_bounds__(256) void k_splat(SplatArgs A) {
     o[4] = ws;
 }
 
-// Four vertically adjacent tile pixels per lane (power-of-two buckets, threshold filter index:
+// NP (4) vertically adjacent tile pixels per lane (power-of-two buckets, threshold filter index:
 // the splat_hits_fast arithmetic).  Consecutive lanes take consecutive tile columns, so a wave's
 // loads of sample i cover contiguous source pixels as in k_splat, and each loaded sample serves
 // up to four pixels (8 source rows x 5 columns per 4 pixels instead of 4 x 25: the splat is
@@ -890,17 +890,18 @@ __global__ __launch_bounds__(256) void k_splat(SplatArgs A) {
 // (source pixel raster, sample) order.  Per-sample work (position, bucket-edge tests, the
 // column test and x distance) is shared.  (Four horizontal pixels per lane measured slower:
 // lanes then read source pixels four apart and the L1 misses rose by a third.)
+template <int NP>
 __global__ __launch_bounds__(256) void k_splat_col4(SplatArgs A) {
     __shared__ float s_table[64];
     __shared__ float s_thr[65];
     if (threadIdx.x < 64) s_table[threadIdx.x] = A.table[threadIdx.x];
     if (threadIdx.x < 65) s_thr[threadIdx.x] = A.thr[threadIdx.x];
     __syncthreads();
-    const uint32_t gpc = (A.tile + 3) / 4, lpb = A.tile * gpc;  // lane groups per tile column / bucket
+    const uint32_t gpc = (A.tile + NP - 1) / NP, lpb = A.tile * gpc;  // lane groups per tile column / bucket
     const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (uint64_t)A.n_buckets * lpb) return;
     const uint32_t bi = (uint32_t)(gid / lpb), rem = (uint32_t)(gid % lpb);
-    const uint32_t tx = rem % A.tile, ty0 = (rem / A.tile) * 4;
+    const uint32_t tx = rem % A.tile, ty0 = (rem / A.tile) * NP;
     const uint32_t bid = A.bucket_ids[bi];
     const uint32_t bx = bid % A.nbx, by = bid / A.nbx;
     const uint32_t x0 = A.B * bx, y0 = A.B * by;
@@ -912,12 +913,12 @@ __global__ __launch_bounds__(256) void k_splat_col4(SplatArgs A) {
     const int sxlo = max(0, (int)tx - fb - r), sxhi = min(bw - 1, (int)tx - fb + r);
     const bool wrapx = bw == (int)A.B && (int)tx <= fb + r + 1 && bw - 1 > sxhi;
     const int ncol = (sxhi >= sxlo ? sxhi - sxlo + 1 : 0) + (wrapx ? 1 : 0);
-    int lo[4], hi[4];
-    bool val[4], wr[4];
+    int lo[NP], hi[NP];
+    bool val[NP], wr[NP];
     int ulo = 1 << 30, uhi = -1;
     bool anywrap = false;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NP; ++j) {
         const int ty = (int)ty0 + j;
         val[j] = ty < (int)A.tile;
         lo[j] = max(0, ty - fb - r);
@@ -935,16 +936,16 @@ __global__ __launch_bounds__(256) void k_splat_col4(SplatArgs A) {
     const float xsA = (float)(tx + x0), xsB = (float)(tx + x0 + A.B);
     const float ysA0 = (float)(ty0 + y0), ysB0 = (float)(ty0 + y0 + A.B);
     const float edgeX = (float)(x0 + A.B + A.fb), edgeY = (float)(y0 + A.B + A.fb);
-    float c[4][5];
+    float c[NP][5];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < NP; ++j)
 #pragma unroll
         for (int k = 0; k < 5; ++k) c[j][k] = 0.f;
     for (int ri = 0; ri < nrow; ++ri) {
         const int sy = (ulo + ri <= uhi) ? ulo + ri : bh - 1;
-        bool act[4];
+        bool act[NP];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) act[j] = val[j] && ((sy >= lo[j] && sy <= hi[j]) || (wr[j] && sy == bh - 1));
+        for (int j = 0; j < NP; ++j) act[j] = val[j] && ((sy >= lo[j] && sy <= hi[j]) || (wr[j] && sy == bh - 1));
         const float fy = (float)(y0 + (uint32_t)sy + A.fb);
         for (int ci = 0; ci < ncol; ++ci) {
             const int sx = (sxlo + ci <= sxhi) ? sxlo + ci : bw - 1;
@@ -961,7 +962,7 @@ __global__ __launch_bounds__(256) void k_splat_col4(SplatArgs A) {
                 const float yb = scy >= edgeY ? ysB0 : ysA0;
                 const float loy = scy - fw, hiy = scy + fw;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < NP; ++j) {
                     if (!act[j]) continue;
                     const float ys = yb + (float)j;
                     const bool hit = xhit && loy < ys + 1.f && ys < hiy;
@@ -1019,7 +1020,7 @@ __global__ __launch_bounds__(256) void k_splat_col4(SplatArgs A) {
     }
     const uint32_t tpx = A.tile * A.tile;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NP; ++j) {
         if (!val[j]) continue;
         float* o = A.tiles + ((uint64_t)bi * tpx + (ty0 + j) * A.tile + tx) * 5;
 #pragma unroll

@@ -867,9 +867,12 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
             std::getenv("NART_SPLAT_LDS") ? std::strtoull(std::getenv("NART_SPLAT_LDS"), nullptr, 10) : 0;
         static const int splat_mode = std::getenv("NART_SPLAT_MODE") ? std::atoi(std::getenv("NART_SPLAT_MODE")) : 3;
         const dim3 sg((uint32_t)((nthreads + 255) / 256));
-        const uint64_t n4 = (uint64_t)nbk * g.tile_size * ((g.tile_size + 3) / 4);
+#ifndef NART_SPLAT_NP
+#define NART_SPLAT_NP 4
+#endif
+        const uint64_t n4 = (uint64_t)nbk * g.tile_size * ((g.tile_size + NART_SPLAT_NP - 1) / NART_SPLAT_NP);
         if (sa.thr && sa.invB != 0.f && splat_mode >= 3)
-            hipLaunchKernelGGL(k_splat_col4, dim3((uint32_t)((n4 + 255) / 256)), dim3(256), 0, st, sa);
+            hipLaunchKernelGGL(k_splat_col4<NART_SPLAT_NP>, dim3((uint32_t)((n4 + 255) / 256)), dim3(256), 0, st, sa);
         else if (sa.thr && sa.invB != 0.f && splat_mode >= 2) hipLaunchKernelGGL(k_splat<2>, sg, dim3(256), splat_lds, st, sa);
         else if (sa.thr && splat_mode >= 1) hipLaunchKernelGGL(k_splat<1>, sg, dim3(256), splat_lds, st, sa);
         else hipLaunchKernelGGL(k_splat<0>, sg, dim3(256), splat_lds, st, sa);
