@@ -4,7 +4,7 @@
 // intersected: the reference's integrator never calls Scene::Intersect.
 //
 // One lane per traced pixel walks its spp samples in order on its RNG stream (the same slot
-// layout as k_render); the kernel needs no BVH and no LDS.
+// layout as k_render); the kernel needs no BVH.  Small density grids are staged in LDS.
 #pragma once
 
 #include "kernels.h"
@@ -245,6 +245,14 @@ __global__ __launch_bounds__(256) void k_render_volume(DScene S, RenderArgs A) {
 // li_volume in the same order: the output is bit-identical.
 template <bool COUNT>
 __global__ __launch_bounds__(256) void k_render_volume_sm(DScene S, RenderArgs A) {
+    // A.lds_nodes != 0: the density grid (that many floats) is staged in LDS
+    extern __shared__ float s_dens[];
+    DMedium mloc = S.medium;
+    if (A.lds_nodes) {
+        for (uint32_t i = threadIdx.x; i < A.lds_nodes; i += blockDim.x) s_dens[i] = S.medium.density[i];
+        __syncthreads();
+        mloc.density = s_dens;
+    }
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= A.n_slots) return;
     const uint32_t slot = A.queue ? A.queue[gid] : gid;
@@ -254,7 +262,7 @@ __global__ __launch_bounds__(256) void k_render_volume_sm(DScene S, RenderArgs A
     const uint2 so = A.slot_so[slot];
     const float2* smp = A.samples + so.x;
     float4* out = A.Lout + so.x;
-    const DMedium& m = S.medium;
+    const DMedium& m = mloc;
     const f3 beta = F3(1.f, 1.f, 1.f);
     enum { P_SAMPLE, P_RAY, P_MAJ, P_COLL, P_ESC };
     uint32_t work = 0, s = 0, bounce = 0;

@@ -656,6 +656,11 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     // NART_VOL_SM=0: the per-sample lock-step kernel (A/B timing only; same output)
     static const bool sm = !(std::getenv("NART_VOL_SM") && std::getenv("NART_VOL_SM")[0] == '0');
     RenderArgs b = a;
+    // small density grids (C5: 2x2x2) are read from LDS (NART_VOL_LDS=0: from global memory)
+    static const bool vol_lds = !(std::getenv("NART_VOL_LDS") && std::getenv("NART_VOL_LDS")[0] == '0');
+    const uint32_t nd = ctx->scene.medium.present ? ctx->scene.medium.rx * ctx->scene.medium.ry * ctx->scene.medium.rz : 0;
+    b.lds_nodes = (sm && vol_lds && nd <= 4096u) ? nd : 0u;
+    const size_t dl = (size_t)b.lds_nodes * sizeof(float);
     if (queue_mode() == 2) {
         int cus = 0, per_cu = 0;
         HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
@@ -665,10 +670,10 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
         if (blocks > resident && (double)n / (256.0 * resident) < 12.0 && a.spp > 4) {
             int rc = ensure_queue(ctx, n);
             if (rc) return rc;
-            RenderArgs pb = a;
+            RenderArgs pb = b;
             pb.spp = 4;
             pb.cost = ctx->d_cost;
-            if (sm) hipLaunchKernelGGL((k_render_volume_sm<false>), dim3(blocks), block, 0, st, ctx->scene, pb);
+            if (sm) hipLaunchKernelGGL((k_render_volume_sm<false>), dim3(blocks), block, dl, st, ctx->scene, pb);
             else hipLaunchKernelGGL((k_render_volume<false>), dim3(blocks), block, 0, st, ctx->scene, pb);
             rc = sort_groups_by_cost(ctx, n, ctx->d_queue, st);
             if (rc) return rc;
@@ -676,8 +681,8 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
         }
     }
     if (sm) {
-        if (ctx->counters) hipLaunchKernelGGL((k_render_volume_sm<true>), dim3(blocks), block, 0, st, ctx->scene, b);
-        else hipLaunchKernelGGL((k_render_volume_sm<false>), dim3(blocks), block, 0, st, ctx->scene, b);
+        if (ctx->counters) hipLaunchKernelGGL((k_render_volume_sm<true>), dim3(blocks), block, dl, st, ctx->scene, b);
+        else hipLaunchKernelGGL((k_render_volume_sm<false>), dim3(blocks), block, dl, st, ctx->scene, b);
     } else {
         if (ctx->counters) hipLaunchKernelGGL((k_render_volume<true>), dim3(blocks), block, 0, st, ctx->scene, b);
         else hipLaunchKernelGGL((k_render_volume<false>), dim3(blocks), block, 0, st, ctx->scene, b);
