@@ -9,4 +9,4 @@ for c in c2 c4 c5; do
 done
 timeout -k 10 600 python tools/shard_perf.py --config c3 --ns 1 2 4 8 --reps 2 > "$OUT/shard_c3.log" 2>&1 || exit 1
 timeout -k 10 600 python tools/shard_perf.py --config c5 --ns 1 2 4 8 --reps 1 > "$OUT/shard_c5.log" 2>&1 || exit 1
-tail -4 "$OUT/shard_c3.log" "$OUT/shard_c5.log"
+tail -n 4 "$OUT/shard_c3.log" "$OUT/shard_c5.log"
