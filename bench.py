@@ -95,17 +95,27 @@ def cpu_baseline(scene, p, ids, stride):
 
 
 def load_traffic(tag):
-    """HBM bytes per launch of the render kernel from the committed rocprofv3 PMC summary."""
+    """HBM bytes per launch of the render kernel (rocprofv3 FETCH_SIZE + WRITE_SIZE, separate
+    --pmc passes of this bench command: tools/profile.sh + tools/summarize_prof.py) and where
+    the figure comes from.  A bench cannot run rocprofv3 on itself, so the figure is read from
+    the committed summary, and only if that summary was measured on the current kernel sources
+    (hip_source_sha); otherwise traffic is null and the source says why."""
+    from nart_amd.build import hip_source_sha
     path = os.path.join(REPO, "profiles", "pmc_latest.json")
     if not os.path.exists(path):
-        return None
+        return None, "no committed PMC summary"
     try:
         d = json.load(open(path))
-        if d.get("config") == tag:
-            return d.get("hbm_bytes_per_launch")
-    except Exception:
-        return None
-    return None
+    except Exception as e:
+        return None, "unreadable PMC summary: %s" % e
+    if d.get("config") != tag:
+        return None, "PMC summary is for %s, not %s" % (d.get("config"), tag)
+    sha = hip_source_sha()
+    if d.get("hip_source_sha") != sha:
+        return None, "PMC summary %s predates the current kernel sources (%s vs %s)" % (
+            d.get("profile"), d.get("hip_source_sha"), sha)
+    return d.get("hbm_bytes_per_launch"), "profiles/%s_pmc.json (rocprofv3 FETCH_SIZE + WRITE_SIZE, kernel sources %s)" % (
+        d.get("profile"), sha)
 
 
 def main():
@@ -190,9 +200,23 @@ def main():
     bps = bytes_per_sample(counters)
     per_launch_samples = st.traced_samples / max(1, st.kernel_launches)
     achieved = bps * per_launch_samples / (kernel_avg_ms * 1e-3) / 1e9
+    traffic, traffic_src = load_traffic("%dx%dx%d" % (W, H, SPP))
+    # achieved/frac price the kernel's ALGORITHMIC bytes (BVH nodes, triangles,
+    # path state per sample) against HBM peak, as the bench contract asks.  Those bytes are
+    # served mostly from LDS/L1/L2 (a ~0.5 MB scene); the kernel is latency/VALU-bound, which
+    # measured_frac (PMC bytes actually moved over HBM / kernel time / peak) shows.
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "achieved_kind": "algorithmic bytes per launch (SURVEY.md 8(d) per-sample model x traced samples)",
+                "limiter": "latency/VALU issue: dependent LDS/L2 loads in BVH traversal, divergent lanes "
+                           "(DESIGN.md section 4), not HBM bandwidth",
+                "measured_frac": (round(traffic / (kernel_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+                                  if traffic else None),
+                "traffic_source": traffic_src,
+                "kernel": "k_render_volume_sm" if p.integrator == 1 else "k_render",
+                "kernel_avg_ms": round(kernel_avg_ms, 3), "bytes_per_sample": round(bps, 1)}
     if rank == 0:
         img_ok = bool(torch.isfinite(image).all().item())
-        volume = p.integrator == 1
         out = {
             "metric": "Msamples/s at %dx%dx%dspp (%s)" % (W, H, SPP, os.path.basename(path)),
             "value": round(value, 3),
@@ -208,11 +232,7 @@ def main():
             "data": cfg["data"],
             "config": {"workload": cfg["workload"], "image": [W, H], "spp": SPP, "buckets": nb,
                        "parallelism": "buckets interleaved over %d rank(s), RCCL gather to rank 0" % world},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": load_traffic("%dx%dx%d" % (W, H, SPP)),
-                         "kernel": "k_render_volume" if volume else "k_render",
-                         "kernel_avg_ms": round(kernel_avg_ms, 3), "bytes_per_sample": round(bps, 1)},
+            "roofline": roofline,
             "kernel_ms_per_step": round(st.kernel_ms / a.steps, 3),
             "splat_ms_per_step": round(st.splat_ms / a.steps, 3),
             "latin_ms_per_step": round(st.latin_ms / a.steps, 3),

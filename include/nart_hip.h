@@ -84,6 +84,18 @@ int nart_hip_eval_sincos(nart_ctx* ctx, const float* x, uint32_t n, float* sin_o
    them (the splat then evaluates sqrt and division per pair). */
 int nart_hip_splat_thresholds(float filter_width, float* thr65);
 
+/* Acceleration structure the context would build for a scene (host only, no device): BVH2 node
+   count, traversal stack depth (levels; the device keeps 8 B per level per lane in LDS) and the
+   triangles in leaves.  Deep trees are capped (median splits past 40 levels), so stack_depth
+   stays <= 72; nart_hip_create returns NART_E_UNSUPPORTED if the stack would not fit in LDS. */
+typedef struct nart_bvh_info {
+    uint32_t num_nodes;
+    uint32_t stack_depth;
+    uint32_t num_leaf_tris;
+    uint32_t reserved;
+} nart_bvh_info;
+int nart_hip_bvh_info(const nart_scene_blob* scene, nart_bvh_info* out);
+
 /* Kernel variant: 0 = megakernel (one lane per pixel slot; traversal quorum on when the launch
    spans >= 3 rounds of resident waves), 1 = wavefront (ray queues), 2 = megakernel with the
    traversal quorum on for every launch (parity tests of that path at small sizes). */

@@ -52,6 +52,12 @@ class SessionGeometry(ctypes.Structure):
                 ("total_height", ctypes.c_uint32), ("n_buckets_x", ctypes.c_uint32), ("n_buckets_y", ctypes.c_uint32)]
 
 
+class BvhInfo(ctypes.Structure):
+    """nart_bvh_info (include/nart_hip.h)."""
+    _fields_ = [("num_nodes", ctypes.c_uint32), ("stack_depth", ctypes.c_uint32), ("num_leaf_tris", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
 class RenderStats(ctypes.Structure):
     _fields_ = [("render_ms", ctypes.c_double), ("kernel_ms", ctypes.c_double), ("splat_ms", ctypes.c_double),
                 ("kernel_launches", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("samples", ctypes.c_uint64),
@@ -98,6 +104,7 @@ _HIP_SIGS = {
     "nart_hip_eval_sincos": (ctypes.c_int, [_P, _P, ctypes.c_uint32, _P, _P]),
     "nart_hip_set_variant": (ctypes.c_int, [_P, ctypes.c_int]),
     "nart_hip_splat_thresholds": (ctypes.c_int, [ctypes.c_float, _P]),
+    "nart_hip_bvh_info": (ctypes.c_int, [_P, ctypes.POINTER(BvhInfo)]),
 }
 SCENE_SYMBOLS = tuple(_SCENE_SIGS)
 HIP_SYMBOLS = tuple(_HIP_SIGS)
@@ -206,6 +213,15 @@ def read_exr(path):
     halves = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint16)), shape=(n,)).copy()
     lib.nart_free(ptr)
     return halves.view(np.float16).astype(np.float32).reshape(h.value, w.value, 4)
+
+
+def bvh_info(scene):
+    """Host only: the BVH a render context would build for `scene` (nart_hip_bvh_info)."""
+    info = BvhInfo()
+    rc = hip_lib().nart_hip_bvh_info(_P(scene.blob), ctypes.byref(info))
+    if rc != NART_OK:
+        raise NartError(rc, "nart_hip_bvh_info")
+    return {"num_nodes": info.num_nodes, "stack_depth": info.stack_depth, "num_leaf_tris": info.num_leaf_tris}
 
 
 class Scene:

@@ -46,6 +46,18 @@ def _sources(*rel):
     return out
 
 
+def hip_source_sha():
+    """sha256 (16 hex digits) of the sources of libnart_hip.so: ties a committed profile (e.g.
+    profiles/pmc_latest.json's HBM traffic) to the kernel code it was measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in _sources("render.hip", "device", "host/bvh_build.cpp", "host/bvh_build.h"):
+        h.update(os.path.relpath(f, CSRC).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def build_scene_lib(force=False):
     os.makedirs(LIB, exist_ok=True)
     out = os.path.join(LIB, "libnart_scene.so")

@@ -76,6 +76,13 @@ ND Ray cast_ray(const DScene& S, f2 smp, uint32_t W, uint32_t H, uint32_t x, uin
     return make_ray(xyz(o), xyz(d));
 }
 
+// Where a slot's samples live: sample s at first + s * stride.  64-bit, since one batch may hold
+// more than 2^32 samples (e.g. 1024x1024-pixel buckets at 4096 spp: 4.3 G samples, 103 GB).
+struct SlotSO {
+    unsigned long long first;
+    uint32_t stride, pad;
+};
+
 struct RenderArgs {
     const uint32_t* slot_xy;  // traced pixel (x | y << 16) in image coordinates
     const float2* samples;    // LatinSquare image samples, sample s of slot at slot_so (sample_index)
@@ -84,7 +91,7 @@ struct RenderArgs {
     // [slot] {first sample index, sample stride}.  Bucket renders lay each bucket out sample-major
     // ([bucket][s][pixel of bucket]: the splat's lanes then read neighbouring pixels' sample s
     // from one cache line); the per-sample API uses {slot * spp, 1}.
-    const uint2* slot_so;
+    const SlotSO* slot_so;
     uint32_t n_slots, spp, bounces, W, H, totalW, stack_depth;
     float gamma;              // roughening factor squared (pathintegrator.cpp:163)
     unsigned long long* counters;  // [5] extend rays, shadow rays, node visits, tri tests, bounces
@@ -97,9 +104,9 @@ struct RenderArgs {
     uint32_t* cost = nullptr; // cost probe: per-slot work estimate of the rendered sample(s)
 };
 
-ND uint32_t sample_index(const RenderArgs& A, uint32_t slot, uint32_t s) {
-    const uint2 so = A.slot_so[slot];
-    return so.x + s * so.y;
+ND size_t sample_index(const RenderArgs& A, uint32_t slot, uint32_t s) {
+    const SlotSO so = A.slot_so[slot];
+    return so.first + (size_t)s * so.stride;
 }
 
 // Stage the top BVH nodes (breadth-first prefix) into LDS; every thread of the block calls it.
@@ -116,24 +123,24 @@ __global__ __launch_bounds__(256) void k_latin(RenderArgs A) {
     uint32_t xy = A.slot_xy[slot];
     uint32_t x = xy & 0xFFFFu, y = xy >> 16;
     uint32_t rng = (y * A.totalW + x) + 2463534242u;  // RNG::Seed (rng.h:10-13)
-    const uint2 so = A.slot_so[slot];
-    float2* s = const_cast<float2*>(A.samples) + so.x;
-    const uint32_t n = A.spp, st = so.y;
+    const SlotSO so = A.slot_so[slot];
+    float2* s = const_cast<float2*>(A.samples) + so.first;
+    const uint32_t n = A.spp, st = so.stride;
     const float inv = 1.f / (float)n;
     for (uint32_t i = 0; i < n; ++i) {
         float a = ((float)i + rng_float(rng)) * inv;  // StratifiedSample1D, x drawn first (Q2)
         float b = ((float)i + rng_float(rng)) * inv;
-        s[i * st] = make_float2(a, b);
+        s[(size_t)i * st] = make_float2(a, b);
     }
     for (uint32_t i = 0; i < n; ++i) {
         uint32_t c = rng_int(rng, n - 1 - i);
-        float t = s[i * st].x;
-        s[i * st].x = s[c * st].x;
-        s[c * st].x = t;
+        float t = s[(size_t)i * st].x;
+        s[(size_t)i * st].x = s[(size_t)c * st].x;
+        s[(size_t)c * st].x = t;
         c = rng_int(rng, n - 1 - i);
-        t = s[i * st].y;
-        s[i * st].y = s[c * st].y;
-        s[c * st].y = t;
+        t = s[(size_t)i * st].y;
+        s[(size_t)i * st].y = s[(size_t)c * st].y;
+        s[(size_t)c * st].y = t;
     }
     const_cast<uint32_t*>(A.rng0)[slot] = rng;
 }
@@ -166,9 +173,9 @@ __global__ __launch_bounds__(64) void k_latin_lds(RenderArgs A) {
         ys[i * 64] = ys[c * 64];
         ys[c * 64] = t;
     }
-    const uint2 so = A.slot_so[slot];
-    float2* s = const_cast<float2*>(A.samples) + so.x;
-    for (uint32_t i = 0; i < n; ++i) s[i * so.y] = make_float2(xs[i * 64], ys[i * 64]);
+    const SlotSO so = A.slot_so[slot];
+    float2* s = const_cast<float2*>(A.samples) + so.first;
+    for (uint32_t i = 0; i < n; ++i) s[(size_t)i * so.stride] = make_float2(xs[i * 64], ys[i * 64]);
     const_cast<uint32_t*>(A.rng0)[slot] = rng;
 }
 
@@ -196,8 +203,8 @@ __global__ __launch_bounds__(64) void k_latin_idx(RenderArgs A, float* scratch) 
         vy[(size_t)i * 64] = ((float)i + rng_float(rng)) * inv;
     }
     const uint32_t rng_gen = rng;
-    const uint2 so = A.slot_so[slot];
-    float2* s = const_cast<float2*>(A.samples) + so.x;
+    const SlotSO so = A.slot_so[slot];
+    float2* s = const_cast<float2*>(A.samples) + so.first;
     uint16_t* ix = s_idx + lane;
     uint16_t* iy = s_idx + (size_t)n * 64 + lane;
     for (int pass = 0; pass < (both ? 1 : 2); ++pass) {
@@ -234,15 +241,15 @@ __global__ __launch_bounds__(64) void k_latin_idx(RenderArgs A, float* scratch) 
             }
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
-                if (both) s[(i + u) * so.y] = make_float2(gx[u], gy[u]);
-                else if (dx) s[(i + u) * so.y].x = gx[u];
-                else s[(i + u) * so.y].y = gy[u];
+                if (both) s[(size_t)(i + u) * so.stride] = make_float2(gx[u], gy[u]);
+                else if (dx) s[(size_t)(i + u) * so.stride].x = gx[u];
+                else s[(size_t)(i + u) * so.stride].y = gy[u];
             }
         }
         for (; i < n; ++i) {
-            if (both) s[i * so.y] = make_float2(vx[(size_t)ix[i * 64] * 64], vy[(size_t)iy[i * 64] * 64]);
-            else if (dx) s[i * so.y].x = vx[(size_t)ix[i * 64] * 64];
-            else s[i * so.y].y = vy[(size_t)ix[i * 64] * 64];
+            if (both) s[(size_t)i * so.stride] = make_float2(vx[(size_t)ix[i * 64] * 64], vy[(size_t)iy[i * 64] * 64]);
+            else if (dx) s[(size_t)i * so.stride].x = vx[(size_t)ix[i * 64] * 64];
+            else s[(size_t)i * so.stride].y = vy[(size_t)ix[i * 64] * 64];
         }
     }
     const_cast<uint32_t*>(A.rng0)[slot] = rng;
@@ -299,7 +306,8 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
     } else if (slot >= A.n_slots) {
         return;
     }
-    uint32_t px = 0, py = 0, rng = 0, soff = 0, sstr = 0;
+    uint32_t px = 0, py = 0, rng = 0, sstr = 0;
+    uint64_t soff = 0;  // first sample index (64-bit: a batch may hold more than 2^32 samples)
     const float2* smp = A.samples;
     float4* out = A.Lout;
     auto take_pixel = [&](uint32_t sl) {
@@ -308,9 +316,9 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
         px = xy & 0xFFFFu;
         py = xy >> 16;
         rng = A.rng0[sl];
-        const uint2 so = A.slot_so[sl];
-        soff = so.x;
-        sstr = so.y;
+        const SlotSO so = A.slot_so[sl];
+        soff = so.first;
+        sstr = so.stride;
     };
     if (slot != 0xFFFFFFFFu) take_pixel(slot);
     int* sc = s_code + tid;
@@ -371,7 +379,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
         ++iters;
         if (new_sample) {
             if (s >= A.spp) break;
-            float2 sm = smp[soff + s * sstr];
+            float2 sm = smp[soff + (uint64_t)s * sstr];
             ray = cast_ray(S, F2(sm.x, sm.y), A.W, A.H, px, py);
             L = F3(0.f, 0.f, 0.f);
             alpha = 0.f;
@@ -390,7 +398,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
         if (new_bounce) {
             new_bounce = false;
             if (bounce >= A.bounces) {
-                out[soff + s * sstr] = make_float4(L.x, L.y, L.z, alpha);
+                out[soff + (uint64_t)s * sstr] = make_float4(L.x, L.y, L.z, alpha);
                 ++s;
                 new_sample = true;
                 continue;
@@ -474,7 +482,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
                 // escaped: at bounce 0 the light seen directly is the result; at bounce > 0 the
                 // reference repeats the same miss until the loop ends (no RNG, no state change)
                 if (bounce == 0 && lightHit) L = Le;
-                out[soff + s * sstr] = make_float4(L.x, L.y, L.z, alpha);
+                out[soff + (uint64_t)s * sstr] = make_float4(L.x, L.y, L.z, alpha);
                 ++s;
                 new_sample = true;
                 continue;
@@ -618,7 +626,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
                 ray = nxt;
                 new_bounce = true;
             } else {
-                out[soff + s * sstr] = make_float4(L.x, L.y, L.z, alpha);
+                out[soff + (uint64_t)s * sstr] = make_float4(L.x, L.y, L.z, alpha);
                 ++s;
                 new_sample = true;
             }
@@ -830,22 +838,22 @@ __global__ __launch_bounds__(256) void k_splat(SplatArgs A) {
             float2 nu0, nu1, nu2, nu3;
             float4 nL0, nL1, nL2, nL3;
             if (A.spp >= 4) {
-                nu0 = sp[0], nu1 = sp[npx], nu2 = sp[2 * npx], nu3 = sp[3 * npx];
-                nL0 = lp[0], nL1 = lp[npx], nL2 = lp[2 * npx], nL3 = lp[3 * npx];
+                nu0 = sp[0], nu1 = sp[npx], nu2 = sp[(size_t)2 * npx], nu3 = sp[(size_t)3 * npx];
+                nL0 = lp[0], nL1 = lp[npx], nL2 = lp[(size_t)2 * npx], nL3 = lp[(size_t)3 * npx];
             }
             for (; i + 4 <= A.spp; i += 4) {
                 const float2 uv0 = nu0, uv1 = nu1, uv2 = nu2, uv3 = nu3;
                 const float4 L0 = nL0, L1 = nL1, L2 = nL2, L3 = nL3;
                 if (i + 8 <= A.spp) {
                     const size_t k0 = (size_t)(i + 4) * npx;
-                    nu0 = sp[k0], nu1 = sp[k0 + npx], nu2 = sp[k0 + 2 * npx], nu3 = sp[k0 + 3 * npx];
-                    nL0 = lp[k0], nL1 = lp[k0 + npx], nL2 = lp[k0 + 2 * npx], nL3 = lp[k0 + 3 * npx];
+                    nu0 = sp[k0], nu1 = sp[k0 + npx], nu2 = sp[k0 + (size_t)2 * npx], nu3 = sp[k0 + (size_t)3 * npx];
+                    nL0 = lp[k0], nL1 = lp[k0 + npx], nL2 = lp[k0 + (size_t)2 * npx], nL3 = lp[k0 + (size_t)3 * npx];
                 }
 #else
             for (; i + 4 <= A.spp; i += 4) {
                 const size_t k0 = (size_t)i * npx;
-                float2 uv0 = sp[k0], uv1 = sp[k0 + npx], uv2 = sp[k0 + 2 * npx], uv3 = sp[k0 + 3 * npx];
-                float4 L0 = lp[k0], L1 = lp[k0 + npx], L2 = lp[k0 + 2 * npx], L3 = lp[k0 + 3 * npx];
+                float2 uv0 = sp[k0], uv1 = sp[k0 + npx], uv2 = sp[k0 + (size_t)2 * npx], uv3 = sp[k0 + (size_t)3 * npx];
+                float4 L0 = lp[k0], L1 = lp[k0 + npx], L2 = lp[k0 + (size_t)2 * npx], L3 = lp[k0 + (size_t)3 * npx];
 #endif
                 float w0, w1, w2, w3;
                 bool h0 = NART_SPLAT_HITS(fx + uv0.x, fy + uv0.y, w0);

@@ -218,15 +218,15 @@ __global__ __launch_bounds__(256) void k_render_volume(DScene S, RenderArgs A) {
     const uint32_t xy = A.slot_xy[slot];
     const uint32_t px = xy & 0xFFFFu, py = xy >> 16;
     uint32_t rng = A.rng0[slot];
-    const uint2 so = A.slot_so[slot];
-    const float2* smp = A.samples + so.x;
-    float4* out = A.Lout + so.x;
+    const SlotSO so = A.slot_so[slot];
+    const float2* smp = A.samples + so.first;
+    float4* out = A.Lout + so.first;
     uint32_t work = 0;
     for (uint32_t s = 0; s < A.spp; ++s) {
-        const float2 sm = smp[s * so.y];
+        const float2 sm = smp[(size_t)s * so.stride];
         const Ray r = cast_ray(S, F2(sm.x, sm.y), A.W, A.H, px, py);
         const f4 L = li_volume(S, A, rng, r.o, r.d, work);
-        out[s * so.y] = make_float4(L.x, L.y, L.z, L.w);
+        out[(size_t)s * so.stride] = make_float4(L.x, L.y, L.z, L.w);
     }
     if (A.cost) {
         A.cost[gid] = work + A.spp;
@@ -259,9 +259,9 @@ __global__ __launch_bounds__(256) void k_render_volume_sm(DScene S, RenderArgs A
     const uint32_t xy = A.slot_xy[slot];
     const uint32_t px = xy & 0xFFFFu, py = xy >> 16;
     uint32_t rng = A.rng0[slot];
-    const uint2 so = A.slot_so[slot];
-    const float2* smp = A.samples + so.x;
-    float4* out = A.Lout + so.x;
+    const SlotSO so = A.slot_so[slot];
+    const float2* smp = A.samples + so.first;
+    float4* out = A.Lout + so.first;
     const DMedium& m = mloc;
     const f3 beta = F3(1.f, 1.f, 1.f);
     enum { P_SAMPLE, P_RAY, P_MAJ, P_COLL, P_ESC };
@@ -274,7 +274,7 @@ __global__ __launch_bounds__(256) void k_render_volume_sm(DScene S, RenderArgs A
         bool finish = false;
         if (ph == P_SAMPLE) {
             if (s >= A.spp) break;
-            const float2 sm = smp[s * so.y];
+            const float2 sm = smp[(size_t)s * so.stride];
             const Ray r = cast_ray(S, F2(sm.x, sm.y), A.W, A.H, px, py);
             o = r.o;
             d = r.d;
@@ -355,7 +355,7 @@ __global__ __launch_bounds__(256) void k_render_volume_sm(DScene S, RenderArgs A
             finish = true;
         }
         if (finish) {
-            out[s * so.y] = make_float4(L.x, L.y, L.z, 1.f);
+            out[(size_t)s * so.stride] = make_float4(L.x, L.y, L.z, 1.f);
             ++s;
             ph = P_SAMPLE;
         }

@@ -276,6 +276,11 @@ struct Builder {
     uint32_t kLeafTarget = 4;   // NART_BVH_LEAF: always a leaf at or below this many triangles
     uint32_t kLeafSah = 8;      // NART_BVH_LEAF_SAH: SAH may stop splitting at or below this
     float kTrav = 1.0f;         // NART_BVH_TRAV: node-visit cost relative to one triangle test
+    // Depth cap.  Binned SAH can peel one bin per level off clustered or graded geometry, and
+    // the traversal stack (8 B per level per lane, 256 lanes per block) lives in LDS.  From this
+    // depth on, nodes split at the object median of the widest centroid axis, so the tree stays
+    // below kMedianDepth + log2(triangles) <= 72 levels (stack <= 144 KiB per block).
+    uint32_t kMedianDepth = 40;  // NART_BVH_MEDIAN_DEPTH
 
     int32_t make_leaf(uint32_t first, uint32_t count) {
         uint32_t leaf_first = (uint32_t)order.size();
@@ -292,6 +297,7 @@ struct Builder {
         if (count <= kLeafTarget) return make_leaf(first, count);
         Box cb;
         for (uint32_t i = first; i < first + count; ++i) cb.grow(tris[i].c, tris[i].c);
+        if (depth >= kMedianDepth) return inner(first, count, depth, median_split(first, count, cb));
         int axis = -1;
         int split_bin = -1;
         float best = std::numeric_limits<float>::infinity();
@@ -350,6 +356,21 @@ struct Builder {
             mid = first + count / 2;  // identical centroids: split by index
         }
         if (mid == first || mid == first + count) mid = first + count / 2;
+        return inner(first, count, depth, mid);
+    }
+    // object median of the widest centroid axis (index order when every centroid coincides)
+    uint32_t median_split(uint32_t first, uint32_t count, const Box& cb) {
+        int axis = 0;
+        for (int a = 1; a < 3; ++a)
+            if (cb.hi[a] - cb.lo[a] > cb.hi[axis] - cb.lo[axis]) axis = a;
+        const uint32_t mid = first + count / 2;
+        if (cb.hi[axis] - cb.lo[axis] > 0.f)
+            std::nth_element(tris.begin() + first, tris.begin() + mid, tris.begin() + first + count,
+                             [axis](const BTri& x, const BTri& y) { return x.c[axis] < y.c[axis]; });
+        return mid;
+    }
+    // inner node over [first, mid) and [mid, first + count)
+    int32_t inner(uint32_t first, uint32_t count, uint32_t depth, uint32_t mid) {
         int32_t idx = (int32_t)out.nodes.size();
         out.nodes.emplace_back();
         out.max_stack = std::max(out.max_stack, depth + 1);
@@ -395,6 +416,7 @@ void build_bvh(const nart_scene_blob& blob, const std::vector<uint8_t>& mask, fl
     if (const char* e = std::getenv("NART_BVH_LEAF")) bld.kLeafTarget = (uint32_t)std::max(1, std::min(NART_LEAF_MAX, std::atoi(e)));
     if (const char* e = std::getenv("NART_BVH_LEAF_SAH")) bld.kLeafSah = (uint32_t)std::max(1, std::min(NART_LEAF_MAX, std::atoi(e)));
     if (const char* e = std::getenv("NART_BVH_TRAV")) bld.kTrav = (float)std::atof(e);
+    if (const char* e = std::getenv("NART_BVH_MEDIAN_DEPTH")) bld.kMedianDepth = (uint32_t)std::max(1, std::min(40, std::atoi(e)));
     if (tris.empty()) {
         out.root_code = -1;  // never traversed (geometry_visible = 0)
         out.num_leaf_tris = 0;

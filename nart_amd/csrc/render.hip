@@ -51,7 +51,7 @@ struct nart_ctx {
     // work buffers
     size_t cap_slot_bytes = 0, cap_misc = 0;
     uint32_t* d_slot_xy = nullptr;
-    uint2* d_slot_so = nullptr;  // [slot] {first sample index, sample stride} (RenderArgs::slot_so)
+    SlotSO* d_slot_so = nullptr;  // [slot] {first sample index, sample stride} (RenderArgs::slot_so)
     uint32_t* d_rng = nullptr;
     float2* d_samples = nullptr;
     float4* d_L = nullptr;
@@ -87,10 +87,16 @@ int fail(nart_ctx* c, int code, const std::string& m) {
     if (c) c->err = m;
     return code;
 }
+// On failure the error is also cleared from HIP's sticky last-error state, so that a context whose
+// call failed (e.g. an allocation) renders normally afterwards.
 #define HIPCHK(call)                                                                             \
     do {                                                                                         \
         hipError_t e_ = (call);                                                                  \
-        if (e_ != hipSuccess) return fail(ctx, NART_E_HIP, std::string(#call ": ") + hipGetErrorString(e_)); \
+        if (e_ != hipSuccess) {                                                                  \
+            (void)hipGetLastError();                                                             \
+            return fail(ctx, e_ == hipErrorOutOfMemory ? NART_E_OOM : NART_E_HIP,                \
+                        std::string(#call ": ") + hipGetErrorString(e_));                        \
+        }                                                                                        \
     } while (0)
 
 template <typename T>
@@ -271,35 +277,55 @@ size_t batch_slot_limit(uint32_t spp) {
     return n < 256 ? 256 : n;
 }
 
+// hipMalloc that leaves no sticky error behind: a failed allocation must not make the next
+// render's hipGetLastError() report it.
+int dmalloc(nart_ctx* ctx, void** p, size_t bytes, const char* what) {
+    const hipError_t e = hipMalloc(p, bytes);
+    if (e == hipSuccess) return NART_OK;
+    *p = nullptr;
+    (void)hipGetLastError();
+    return fail(ctx, e == hipErrorOutOfMemory ? NART_E_OOM : NART_E_HIP,
+                std::string("hipMalloc ") + what + " (" + std::to_string(bytes) + " B): " + hipGetErrorString(e));
+}
+
+// Work buffers for a batch.  Each group's capacity is reset before its buffers are freed, so a
+// failed allocation leaves a state in which the next call allocates again (never a stale
+// capacity over null buffers).
 int ensure(nart_ctx* ctx, size_t slots, uint32_t spp, size_t buckets) {
-    size_t samples = slots * spp;
+    const size_t samples = slots * spp;
+    int rc = NART_OK;
     if (slots > ctx->cap_slots) {
-        if (ctx->d_slot_xy) hipFree(ctx->d_slot_xy);
-        if (ctx->d_rng) hipFree(ctx->d_rng);
-        if (ctx->d_slot_so) hipFree(ctx->d_slot_so);
-        ctx->d_slot_xy = nullptr;
-        ctx->d_rng = nullptr;
-        ctx->d_slot_so = nullptr;
-        HIPCHK(hipMalloc(&ctx->d_slot_xy, slots * 4));
-        HIPCHK(hipMalloc(&ctx->d_slot_so, slots * sizeof(uint2)));
-        HIPCHK(hipMalloc(&ctx->d_rng, slots * 4));
+        ctx->cap_slots = 0;
+        for (void** b : {(void**)&ctx->d_slot_xy, (void**)&ctx->d_rng, (void**)&ctx->d_slot_so}) {
+            if (*b) hipFree(*b);
+            *b = nullptr;
+        }
+        if ((rc = dmalloc(ctx, (void**)&ctx->d_slot_xy, slots * 4, "slot pixels")) ||
+            (rc = dmalloc(ctx, (void**)&ctx->d_slot_so, slots * sizeof(SlotSO), "slot sample table")) ||
+            (rc = dmalloc(ctx, (void**)&ctx->d_rng, slots * 4, "slot RNG states")))
+            return rc;
         ctx->cap_slots = slots;
     }
     if (samples > ctx->cap_samples) {
-        if (ctx->d_samples) hipFree(ctx->d_samples);
-        if (ctx->d_L) hipFree(ctx->d_L);
-        ctx->d_samples = nullptr;
-        ctx->d_L = nullptr;
-        HIPCHK(hipMalloc(&ctx->d_samples, samples * sizeof(float2)));
-        HIPCHK(hipMalloc(&ctx->d_L, samples * sizeof(float4)));
+        ctx->cap_samples = 0;
+        for (void** b : {(void**)&ctx->d_samples, (void**)&ctx->d_L}) {
+            if (*b) hipFree(*b);
+            *b = nullptr;
+        }
+        if ((rc = dmalloc(ctx, (void**)&ctx->d_samples, samples * sizeof(float2), "LatinSquare samples")) ||
+            (rc = dmalloc(ctx, (void**)&ctx->d_L, samples * sizeof(float4), "per-sample radiance")))
+            return rc;
         ctx->cap_samples = samples;
     }
     if (buckets > ctx->cap_buckets) {
-        if (ctx->d_bucket_ids) hipFree(ctx->d_bucket_ids);
-        if (ctx->d_bucket_base) hipFree(ctx->d_bucket_base);
-        ctx->d_bucket_ids = ctx->d_bucket_base = nullptr;
-        HIPCHK(hipMalloc(&ctx->d_bucket_ids, buckets * 4));
-        HIPCHK(hipMalloc(&ctx->d_bucket_base, buckets * 4));
+        ctx->cap_buckets = 0;
+        for (void** b : {(void**)&ctx->d_bucket_ids, (void**)&ctx->d_bucket_base}) {
+            if (*b) hipFree(*b);
+            *b = nullptr;
+        }
+        if ((rc = dmalloc(ctx, (void**)&ctx->d_bucket_ids, buckets * 4, "bucket ids")) ||
+            (rc = dmalloc(ctx, (void**)&ctx->d_bucket_base, buckets * 4, "bucket bases")))
+            return rc;
         ctx->cap_buckets = buckets;
     }
     return NART_OK;
@@ -403,15 +429,16 @@ int sort_groups_by_cost(nart_ctx* ctx, uint32_t n, uint32_t* out, hipStream_t st
 
 // Sample-major bucket layout: slot `base + p` of a bucket of `cnt` traced pixels keeps sample s
 // at base*spp + s*cnt + p.  One block per bucket of the batch.
-__global__ void k_slot_table(const uint32_t* bucket_base, uint32_t nbk, uint32_t nslots, uint32_t spp, uint2* so) {
+__global__ void k_slot_table(const uint32_t* bucket_base, uint32_t nbk, uint32_t nslots, uint32_t spp, SlotSO* so) {
     const uint32_t b = blockIdx.x;
     const uint32_t base = bucket_base[b], end = b + 1 < nbk ? bucket_base[b + 1] : nslots;
-    for (uint32_t p = threadIdx.x; base + p < end; p += blockDim.x) so[base + p] = make_uint2(base * spp + p, end - base);
+    for (uint32_t p = threadIdx.x; base + p < end; p += blockDim.x)
+        so[base + p] = SlotSO{(unsigned long long)base * spp + p, end - base, 0u};
 }
 
-__global__ void k_slot_rows(uint32_t n, uint32_t spp, uint2* so) {
+__global__ void k_slot_rows(uint32_t n, uint32_t spp, SlotSO* so) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) so[i] = make_uint2(i * spp, 1u);
+    if (i < n) so[i] = SlotSO{(unsigned long long)i * spp, 1u, 0u};
 }
 
 __global__ void k_iota(uint32_t* v, uint32_t n) {
@@ -558,7 +585,7 @@ int wf_layout(nart_ctx* ctx, uint32_t n, int maxl, WFArgs& w) {
         if (ctx->d_wf) hipFree(ctx->d_wf);
         ctx->d_wf = nullptr;
         ctx->cap_wf = 0;
-        if (hipMalloc(&ctx->d_wf, off) != hipSuccess) return fail(ctx, NART_E_OOM, "hipMalloc wavefront state");
+        if (int rc = dmalloc(ctx, &ctx->d_wf, off, "wavefront state")) return rc;
         ctx->cap_wf = off;
     }
     char* b = static_cast<char*>(ctx->d_wf);
@@ -1009,6 +1036,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     // scale (|o| + |t d| <= 3 * maxabs, errors of a few ulps): octree.h oc_clear
     nart::annotate_octree_leaves(*blob, oct, maxabs * 6.103515625e-05f, bvh);
     ctx->stack_depth = std::max<uint32_t>(bvh.max_stack + 1, 2);
+    if ((size_t)ctx->stack_depth * 256 * 8 > (size_t)160 * 1024) return bail(NART_E_UNSUPPORTED);  // LDS stack
     if ((rc = upload(ctx, ctx->d_nodes, bvh.nodes.data(), bvh.nodes.size()))) return bail(rc);
     ctx->num_nodes = (uint32_t)bvh.nodes.size();
     if ((rc = upload(ctx, ctx->d_tri_isect, bvh.tri_isect.data(), bvh.tri_isect.size()))) return bail(rc);
@@ -1250,6 +1278,21 @@ int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t
     rc = dispatch_render(ctx, ra, p->integrator, 0);
     if (rc) return rc;
     HIPCHK(hipMemcpy(out, ctx->d_L, (size_t)n * p->spp * sizeof(float4), hipMemcpyDeviceToHost));
+    return NART_OK;
+}
+
+int nart_hip_bvh_info(const nart_scene_blob* blob, nart_bvh_info* out) {
+    if (!blob || !out) return NART_E_INVALID;
+    std::vector<uint8_t> mask;
+    bool root_leaf = false;
+    uint32_t n_chunks = 0;
+    nart::reference_visibility(*blob, mask, root_leaf, n_chunks, nullptr);
+    nart::BuiltBVH bvh;
+    nart::build_bvh(*blob, mask, 0.f, bvh);
+    out->num_nodes = (uint32_t)bvh.nodes.size();
+    out->stack_depth = std::max<uint32_t>(bvh.max_stack + 1, 2);  // as nart_hip_create
+    out->num_leaf_tris = bvh.num_leaf_tris;
+    out->reserved = 0;
     return NART_OK;
 }
 

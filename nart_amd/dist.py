@@ -5,7 +5,8 @@ tiles into the image in bucket raster order (render.cpp:152-203).  Across ranks:
   * rank r renders buckets r, r + N, r + 2N, ... (interleaved: the costly sphere region spreads
     evenly over ranks, with no host work queue);
   * each rank's tiles (tileSize^2 Pixels per bucket) are gathered to rank 0 with one
-    torch.distributed gather (RCCL over xGMI on GPUs, gloo in the CPU tests);
+    torch.distributed gather (RCCL over xGMI on GPUs; gloo in the CPU tests, and in the
+    one-GPU multi-rank test, where device tiles are staged through host memory);
   * rank 0 scatters them into bucket-id order and combines in bucket raster order, so the
     image is bit-identical for any N.
 No other collective is on the data path.
@@ -35,10 +36,16 @@ class BucketShard:
         """Collective: rank 0 returns the (n_buckets, tileSize^2, 5) tiles in bucket-id order."""
         if self.world > 1:
             import torch.distributed as td
+            # gloo gathers host tensors only: stage device tiles through host memory
+            stage = self.tiles.is_cuda and td.get_backend() == "gloo"
+            mine = self.tiles.cpu() if stage else self.tiles
             if self.rank == 0:
-                td.gather(self.tiles, gather_list=list(self.gathered.unbind(0)), dst=0)
+                dst = self.gathered.cpu() if stage else self.gathered
+                td.gather(mine, gather_list=list(dst.unbind(0)), dst=0)
+                if stage:
+                    self.gathered.copy_(dst)
             else:
-                td.gather(self.tiles, dst=0)
+                td.gather(mine, dst=0)
                 return None
             src = self.gathered.view(self.world * self.per_rank, self.tpx, 5)
         else:

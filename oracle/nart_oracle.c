@@ -1823,6 +1823,9 @@ void oracle_latin_square(uint32_t seed, uint32_t spp, float* out_xy, uint32_t* s
 }
 
 float oracle_fresnel(float eta_o, float eta_i, float c) { return fresnel(eta_o, eta_i, c); }
+uint32_t oracle_binary_search(float value, const float* v, uint32_t start, uint32_t end) {
+    return binary_search(value, v, start, end);
+}
 
 /* ---------------------------------------------------------------- debugging aids (tests/tools only) */
 /* Camera ray of pixel (x, y) with image sample (u, v) (pinholecamera.cpp:9-40). */

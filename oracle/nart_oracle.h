@@ -52,6 +52,8 @@ int oracle_bvh_stats(const oracle_scene* s, uint32_t* n_chunks, uint32_t* max_ch
 void oracle_rng_stream(uint32_t seed, uint32_t n, float* out);
 void oracle_latin_square(uint32_t seed, uint32_t spp, float* out_xy, uint32_t* rng_state_after);
 float oracle_fresnel(float eta_o, float eta_i, float cos_theta);
+/* BinarySearch (util.cpp:4-20) as the environment light's CDF inversion uses it. */
+uint32_t oracle_binary_search(float value, const float* v, uint32_t start, uint32_t end);
 
 #ifdef __cplusplus
 }

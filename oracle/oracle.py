@@ -18,9 +18,44 @@ def default_threads():
     return max(1, min(16, os.cpu_count() or 1))
 
 
+REF_LIB = os.path.join(HERE, "_ref", "libref_util.so")
+REF_SRC = os.environ.get("NART_REFERENCE", "/root/reference")
+
+
 def build():
     subprocess.check_call(["make", "-s", "-C", HERE])
+    build_ref()
     return LIB
+
+
+def build_ref():
+    """oracle/_ref/libref_util.so: the reference's own util.cpp (BinarySearch), compiled in place
+    from the reference checkout when it is present (this container; the GPU box gets the built
+    file with the tree).  Returns the path, or None without the reference."""
+    if os.path.exists(os.path.join(REF_SRC, "src", "core", "util.cpp")):
+        subprocess.check_call(["make", "-s", "-C", HERE, "ref", "REF=" + REF_SRC])
+    return REF_LIB if os.path.exists(REF_LIB) else None
+
+
+def ref_binary_search():
+    """The reference's BinarySearch (util.cpp:4-20) as f(value, cdf, start, end), or None."""
+    if not os.path.exists(REF_LIB):
+        return None
+    ref = ctypes.CDLL(REF_LIB)
+    ref.ref_binary_search.restype = ctypes.c_uint32
+    ref.ref_binary_search.argtypes = [ctypes.c_float, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.c_uint32]
+
+    def f(value, cdf, start, end):
+        cdf = np.ascontiguousarray(cdf, np.float32)
+        return ref.ref_binary_search(float(value), cdf.ctypes.data, len(cdf), start, end)
+    return f
+
+
+def binary_search(value, cdf, start, end):
+    """The oracle's restatement of BinarySearch (nart_oracle.c)."""
+    cdf = np.ascontiguousarray(cdf, np.float32)
+    return lib().oracle_binary_search(float(value), cdf.ctypes.data, start, end)
 
 
 def lib():
@@ -41,6 +76,8 @@ def lib():
         _lib.oracle_latin_square.argtypes = [ctypes.c_uint32, ctypes.c_uint32, P, P]
         _lib.oracle_fresnel.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_float]
         _lib.oracle_fresnel.restype = ctypes.c_float
+        _lib.oracle_binary_search.argtypes = [ctypes.c_float, P, ctypes.c_uint32, ctypes.c_uint32]
+        _lib.oracle_binary_search.restype = ctypes.c_uint32
         _lib.oracle_camera_ray.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                            ctypes.c_float, ctypes.c_float, P, P]
         _lib.oracle_trace.argtypes = [P, P, P, ctypes.c_float, P]

@@ -70,3 +70,19 @@ def test_splat_thresholds_reproduce_filter_index(built):
         assert np.array_equal(got, want), fw
     thr = np.zeros(65, np.float32)
     assert lib.nart_hip_splat_thresholds(ctypes.c_float(0.1), thr.ctypes.data) != 0
+
+
+def test_bvh_depth_cap(built, glass_scene, monkeypatch):
+    """Host BVH build (nart_hip_bvh_info, no device): binned SAH, and from NART_BVH_MEDIAN_DEPTH
+    on object-median splits, which bound the traversal stack (LDS) by that depth plus
+    log2(triangles / leaf size) -- the guard against SAH peeling one bin per level off clustered
+    geometry.  glassSphere: 2,560 triangles, all visible to the reference octree."""
+    import math
+    info = nart_amd.bvh_info(glass_scene)
+    assert info["num_leaf_tris"] == 2560
+    assert 2 <= info["stack_depth"] <= 72
+    for md in (1, 2, 5):
+        monkeypatch.setenv("NART_BVH_MEDIAN_DEPTH", str(md))
+        capped = nart_amd.bvh_info(glass_scene)
+        assert capped["num_leaf_tris"] == 2560
+        assert capped["stack_depth"] <= md + math.ceil(math.log2(2560 / 4)) + 2, (md, capped)

@@ -1,0 +1,69 @@
+"""Multi-rank data path on the GPU: two ranks on one MI355X, each rendering its interleaved bucket
+share with nart_hip_render_buckets_async into device tiles, the tiles gathered to rank 0
+(nart_amd.dist.BucketShard; gloo staging through host memory, since RCCL needs one GPU per
+rank) and combined on the device.  The image must equal the single-rank render bit for bit.
+This covers everything bench.py's N-GPU path runs except the RCCL transport itself."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, scene_path, w, h, spp, out_path):
+    sys.path[:0] = [REPO]
+    import torch
+    import torch.distributed as td
+    import nart_amd
+    from nart_amd.dist import BucketShard
+    td.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        scene = nart_amd.Scene(scene_path)
+        p = nart_amd.load_sessions(scene_path)[0]
+        p.image_width, p.image_height, p.spp = w, h, spp
+        g = nart_amd.session_geometry(p)
+        nb = g.n_buckets_x * g.n_buckets_y
+        gpu = nart_amd.HipRenderer(scene, device=0)
+        stream = torch.cuda.current_stream()
+        shard = BucketShard(nb, g.tile_size * g.tile_size, rank, world, dev)
+        gpu.render_buckets_async(p, shard.mine, shard.tiles.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize()
+        by_id = shard.gather()
+        if rank == 0:
+            image = torch.zeros((g.total_height, g.total_width, 5), dtype=torch.float32, device=dev)
+            gpu.combine_async(p, by_id.data_ptr(), image.data_ptr(), stream.cuda_stream)
+            torch.cuda.synchronize()
+            np.save(out_path, image.cpu().numpy())
+        td.barrier()
+    finally:
+        td.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ranks_on_one_gpu_match_single_rank(gpu, glass_scene, tmp_path, world):
+    import nart_amd
+    w, h, spp = 200, 120, 8  # 13 x 8 buckets: uneven shares
+    out = str(tmp_path / "img.npy")
+    mp.start_processes(_worker, args=(world, _free_port(), glass_scene.path, w, h, spp, out), nprocs=world,
+                       start_method="spawn")
+    img = np.load(out)
+    p = nart_amd.load_sessions(glass_scene.path)[0]
+    p.image_width, p.image_height, p.spp = w, h, spp
+    ref = nart_amd.HipRenderer(glass_scene).render(p)
+    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))

@@ -34,7 +34,10 @@ def main(src, tag, config="1920x1080x256"):
             dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
             d["launches"].setdefault(r["Dispatch_Id"] if kind == "fetch" else None, None)
             d.setdefault(kind, []).append((float(r["Counter_Value"]), dur))
-    out = {"config": config, "kernels": {}}
+    sys.path.insert(0, REPO)
+    from nart_amd.build import hip_source_sha
+    # the profiled run's kernels are this tree's (run from the same snapshot)
+    out = {"config": config, "profile": tag, "hip_source_sha": hip_source_sha(), "kernels": {}}
     for k, d in per.items():
         f = max(d.get("fetch", [(0, 0)]))
         w = max(d.get("write", [(0, 0)]))
