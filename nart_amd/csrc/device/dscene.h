@@ -107,6 +107,10 @@ static_assert(sizeof(OcNode) == 72, "OcNode must be 72 B");
 struct DScene {
     const BVHNode* nodes;
     const float4* tri_isect;
+    // tri_isect's vertices pre-permuted per ray major axis (Triangle::Intersect's
+    // (kx, ky, kz) = (m+1, m+2, m) mod 3, geometry.cpp:48-56): [major][leaf-order tri] 48 B =
+    // {v0p.xyz, v1p.x}, {v1p.yz, v2p.xy}, {v2p.z, global index, info, grazing threshold}
+    const float4* tri_perm;
     const nart_triangle* tris;
     const uint32_t* tri_mesh;
     const DMesh* meshes;
@@ -117,6 +121,7 @@ struct DScene {
     const DEnvDist* envs;
     uint32_t num_lights;
     uint32_t num_tris;
+    uint32_t num_leaf_tris;  // test records in leaf order (tri_isect, one tri_perm block)
     int32_t root;            // root code (inner node index or leaf code)
     int32_t geometry_visible;// 0 when the reference octree's root is a leaf (bvh.cpp:131, Q14)
     float cam_m[16];

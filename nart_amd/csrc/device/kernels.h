@@ -102,6 +102,8 @@ struct RenderArgs {
     uint32_t* qhead = nullptr;
     uint32_t qbase = 0;
     uint32_t* cost = nullptr; // cost probe: per-slot work estimate of the rendered sample(s)
+    uint32_t rq_quorum = 8;   // k_render_rq: leave a traversal phase once the wave's queue is empty
+                              // and at most this many lanes still trace
 };
 
 ND size_t sample_index(const RenderArgs& A, uint32_t slot, uint32_t s) {
@@ -321,7 +323,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
         sstr = so.stride;
     };
     if (slot != 0xFFFFFFFFu) take_pixel(slot);
-    int* sc = s_code + tid;
+    int* sc = reinterpret_cast<int*>(reinterpret_cast<int2*>(s_dyn) + tid);  // [depth][lane] int2
     float* stn = s_tn + tid;
     const int stride = blockDim.x;
     const float nL = (float)S.num_lights;
@@ -656,13 +658,404 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
         atomicAdd(&wv[5], (unsigned long long)cnt.nodes);
         atomicAdd(&wv[6], (unsigned long long)cnt.pw[4]);
         atomicAdd(&wv[7], (unsigned long long)cnt.tris);
-        for (int i = 0; i < 10; ++i) atomicAdd(&A.counters[8 + i], (unsigned long long)cnt.pw[i]);
+        for (int i = 0; i < 12; ++i) atomicAdd(&A.counters[8 + i], (unsigned long long)cnt.pw[i]);
     }
 #endif
     if (A.cost) {  // cost probe (one pixel per lane, no queue): node/triangle/iteration weights
         A.cost[gid] = cnt.nodes + 2u * cnt.tris + 30u * iters;
         return;
     }
+    if (COUNT) {
+        atomicAdd(&A.counters[0], (unsigned long long)n_ext);
+        atomicAdd(&A.counters[1], (unsigned long long)n_sh);
+        atomicAdd(&A.counters[2], (unsigned long long)cnt.nodes);
+        atomicAdd(&A.counters[3], (unsigned long long)cnt.tris);
+        atomicAdd(&A.counters[4], (unsigned long long)n_bounce);
+        atomicAdd(&A.counters[5], (unsigned long long)cnt.oc_checks);
+        atomicAdd(&A.counters[6], (unsigned long long)cnt.oc_replays);
+    }
+}
+
+// ---------------------------------------------------------------- path tracing with a wave ray queue
+// k_render_rq: the same per-lane path state machine as k_render (one lane per traced pixel,
+// its samples in order on one RNG stream), but the lanes of a wave share their rays.  Shading
+// a hit yields up to three independent queries -- EstimateDirect's two shadow rays and the
+// continuation (whose light-loop bound is known at once) -- because none of their results feeds
+// back into the RNG draws or the continuation.  They go into the wave's LDS outbox; in the
+// traversal phase every lane takes the next queued ray of any lane as soon as its current one
+// resolves, so lanes stay busy until the wave's queue drains instead of idling behind the
+// slowest query of each round.  A path whose results are all in then accumulates the
+// EstimateDirect term in the reference's order ((0 + c1) + c2) * nL * beta, and shades its
+// next hit.  Each lane's operations and their order are those of k_render (bit-identical).
+//
+// LDS per wave: outbox [kind][lane] 32 B {o, tmax}, {d, -} (kind 0 continuation / camera
+// ray, 1 and 2 the shadow rays), results [lane] {ext hit, shadow 1, shadow 2}, and the
+// list of queued (lane, kind) ids of the current traversal phase.
+#define RQ_PENDING 0xFFFFFFFEu
+NHD size_t rq_lds_bytes(uint32_t stack_depth, uint32_t block) {
+    const uint32_t waves = block / 64;
+    return (size_t)stack_depth * block * 8 + (size_t)waves * 3 * 64 * 32 + (size_t)block * 16 + (size_t)waves * 192;
+}
+
+#ifndef NART_RQ_BLOCK
+#define NART_RQ_BLOCK 256
+#endif
+template <int MAXL, bool COUNT, bool ENV>
+__global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(DScene S, RenderArgs A) {
+    extern __shared__ __attribute__((aligned(16))) int s_dyn[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6;
+    const int stride = blockDim.x;
+    const uint32_t nwave = blockDim.x / 64;
+    int2* s_stack = reinterpret_cast<int2*>(s_dyn);
+    float4* s_out = reinterpret_cast<float4*>(s_stack + A.stack_depth * blockDim.x);  // [wave][kind][lane][2]
+    uint4* s_res = reinterpret_cast<uint4*>(s_out + nwave * 3 * 64 * 2);             // [wave*64 + lane]
+    uint8_t* s_list = reinterpret_cast<uint8_t*>(s_res + blockDim.x) + wv * 192;      // this wave's id list
+    float4* s_nodes = reinterpret_cast<float4*>(reinterpret_cast<uint8_t*>(s_res + blockDim.x) + nwave * 192);
+    stage_nodes(S, s_nodes, A.lds_nodes);
+    const int nl = (int)A.lds_nodes;
+    float4* my_out = s_out + (size_t)wv * 3 * 64 * 2;  // kind k, lane l: my_out[(k * 64 + l) * 2]
+    uint4* my_res = s_res + tid;
+    int* sc = reinterpret_cast<int*>(s_stack + tid);
+    const float nL = (float)S.num_lights;
+    const uint32_t gid = blockIdx.x * blockDim.x + tid;
+
+    uint32_t slot = gid;
+    if (A.queue) slot = gid < A.n_slots ? A.queue[gid] : 0xFFFFFFFFu;
+    else if (slot >= A.n_slots) slot = 0xFFFFFFFFu;  // the lane still serves its wave's queue
+    uint32_t px = 0, py = 0, rng = 0, sstr = 0;
+    uint64_t soff = 0;
+    auto take_pixel = [&](uint32_t sl) {
+        slot = sl;
+        const uint32_t xy = A.slot_xy[sl];
+        px = xy & 0xFFFFu;
+        py = xy >> 16;
+        rng = A.rng0[sl];
+        const SlotSO so = A.slot_so[sl];
+        soff = so.first;
+        sstr = so.stride;
+    };
+    if (slot != 0xFFFFFFFFu) take_pixel(slot);
+    uint32_t s = slot != 0xFFFFFFFFu ? 0u : A.spp;
+
+    TraceCounters cnt = {0u, 0u, 0u, 0u};
+    uint32_t n_ext = 0, n_sh = 0, n_bounce = 0;
+    f3 L = F3(0.f, 0.f, 0.f), beta = F3(0.f, 0.f, 0.f), Le = F3(0.f, 0.f, 0.f);
+    f3 c1 = F3(0.f, 0.f, 0.f), c2 = F3(0.f, 0.f, 0.f), betak = F3(0.f, 0.f, 0.f);
+    float alpha = 0.f, eta_sampled = 1.f, eta_outer = 1.f, alphaTweak = 1.f;
+    uint32_t flags = 0, bounce = 0;
+    IList<MAXL> list;
+    list.n = 0;
+    bool lightHit = false, use1 = false, use2 = false, have_ed = false, ext_pending = false;
+    bool waiting = false;  // rays of this lane's path are queued or in flight
+    uint32_t newk = 0;     // rays this lane queued in the current path phase (bit per kind)
+
+    // traversal state of the ray this lane is tracing (any lane's)
+    Trav tq;
+    Ray tr;
+    uint32_t tid8 = 0;  // queued id: owner lane | kind << 6
+    bool tracing = false;
+
+#ifdef NART_WAVEPROF
+    const uint64_t prof_t0 = __builtin_amdgcn_s_memtime();
+#endif
+    auto put_ray = [&](int kind, f3 o, f3 d, float tmax) {
+        float4* e = my_out + (kind * 64 + lane) * 2;
+        e[0] = make_float4(o.x, o.y, o.z, tmax);
+        e[1] = make_float4(d.x, d.y, d.z, 0.f);
+        newk |= 1u << kind;
+    };
+    // light intersections of a new extension ray (pathintegrator.cpp:167-182), then queue it
+    auto queue_ext = [&](f3 o, f3 d) {
+        float lightTMax = __builtin_inff();
+        lightHit = false;
+        Le = F3(0.f, 0.f, 0.f);
+        for (uint32_t j = 0; j < S.num_lights; ++j) {
+            float lt = __builtin_inff();
+            f3 Li = light_li<ENV>(S, S.lights[j], o, d, nullptr, lt);
+            if (lt < lightTMax) {
+                Le = Li;
+                lightTMax = lt;
+                lightHit = true;
+                alpha = 1.f;
+            }
+        }
+        put_ray(0, o, d, lightTMax);
+        ext_pending = true;
+        if (COUNT) ++n_ext;
+    };
+
+    for (;;) {
+        // ---------------- path phase
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        newk = 0;
+#ifdef NART_WAVEPROF
+        if (COUNT && lane == 0) cnt.pw[10]++;  // path phases
+        const uint64_t prof_tp = __builtin_amdgcn_s_memtime();
+#endif
+        if (waiting) {
+            const uint4 r = *my_res;
+            if ((!ext_pending || r.x != RQ_PENDING) && (!use1 || r.y != 2u) && (!use2 || r.z != 2u)) {
+                waiting = false;
+                // L += EstimateDirect(...) * beta, EstimateDirect = ((0 + c1) + c2) * numLights
+                if (have_ed) {
+                    f3 Led = F3(0.f, 0.f, 0.f);
+                    if (use1 && r.y == 0u) Led = add(Led, c1);
+                    if (use2 && r.z == 0u) Led = add(Led, c2);
+                    L = add(L, mul(muls(Led, nL), betak));
+                }
+                bool done = true;
+                if (ext_pending && r.x != NO_HIT) {
+                    // ---- shade the hit (pathintegrator.cpp:185-246)
+                    done = false;
+                    if (COUNT) ++n_bounce;
+                    if (COUNT) WPROF(cnt, 8);
+                    const float4 ro = my_out[lane * 2], rd = my_out[lane * 2 + 1];
+                    const Ray cur = make_ray(F3(ro.x, ro.y, ro.z), F3(rd.x, rd.y, rd.z));
+                    Isect is;
+                    fill_isect(S, cur, r.x, is);
+                    BSDF bsdf;
+                    create_bsdf(S, is, alphaTweak, bsdf);
+                    use1 = use2 = false;
+                    bool cont;
+                    f3 no, nd;
+                    if (list.valid(is.meshID, is.priority, eta_outer)) {
+                        if (bounce == 0) alpha = 1.f;
+                        const f3 wo = to_local(bsdf, neg(cur.d));
+                        // ---- EstimateDirect (pathintegrator.cpp:38-121)
+                        const DLight& Lg = S.lights[f2u8(gmin(rng_float(rng), ND_ONE_MINUS_EPS) * nL)];
+                        float sPdf = 0.f, lPdf = 0.f;
+                        float sx = rng_float(rng);
+                        float sy = rng_float(rng);
+                        float bsmp = rng_float(rng);
+                        uint32_t dflags = 0;
+                        f3 wi;
+                        f3 f = bsdf_sample_f(bsdf, wo, wi, bsmp, F2(sx, sy), sPdf, dflags, true, eta_outer, nullptr,
+                                             nullptr);
+                        if (sPdf > 0.f) {
+                            float flip = wi.z > 0.f ? 1.f : -1.f;
+                            f3 wW = to_world(bsdf, wi);
+                            float lt = __builtin_inff();
+                            f3 Li = light_li<ENV>(S, Lg, is.p, wW, &lPdf, lt);
+                            float weight = 1.f;
+                            bool add1 = true;
+                            if (!(dflags & F_SPECULAR)) {
+                                weight = (sPdf * sPdf) / (sPdf * sPdf + lPdf * lPdf);
+                                add1 = lPdf > 0.f;
+                            }
+                            if (add1) {
+                                c1 = divs(muls(muls(mul(f, Li), gabs(wi.z)), weight), sPdf);
+                                // an all-zero term cannot change the sum: skip its shadow ray
+                                use1 = !(c1.x == 0.f && c1.y == 0.f && c1.z == 0.f);
+                                if (use1) put_ray(1, add(is.p, muls(muls(is.gn, SHADOW_BIAS), flip)), wW, lt);
+                            }
+                        }
+                        lPdf = 0.f;
+                        float lx = rng_float(rng);
+                        float ly = rng_float(rng);
+                        f3 wiW;
+                        float lt2 = __builtin_inff();
+                        f3 Li2 = light_sample_li<ENV>(S, Lg, is.p, wiW, F2(lx, ly), lPdf, lt2);
+                        f3 wi2 = to_local(bsdf, wiW);
+                        if (lPdf > 0.f) {
+                            float sp2 = bsdf_pdf(bsdf, wo, wi2, true, eta_outer);
+                            if (sp2 > 0.f) {
+                                f3 fv = bsdf_f(bsdf, wo, wi2, true, eta_outer);
+                                float weight = (lPdf * lPdf) / (sp2 * sp2 + lPdf * lPdf);
+                                c2 = divs(muls(muls(mul(fv, Li2), gabs(wi2.z)), weight), lPdf);
+                                use2 = !(c2.x == 0.f && c2.y == 0.f && c2.z == 0.f);
+                                if (use2) {
+                                    float flip2 = wi2.z > 0.f ? 1.f : -1.f;
+                                    put_ray(2, add(is.p, muls(muls(is.gn, SHADOW_BIAS), flip2)), wiW, lt2);
+                                }
+                            }
+                        }
+                        betak = beta;
+                        have_ed = true;
+                        // ---- continuation (pathintegrator.cpp:199-220)
+                        float a = rng_float(rng);
+                        float b = rng_float(rng);
+                        float bs2 = rng_float(rng);
+                        float cpdf = 0.f, alpha_i = 0.f;
+                        f3 wic;
+                        f3 fc = bsdf_sample_f(bsdf, wo, wic, bs2, F2(a, b), cpdf, flags, false, eta_outer, &alpha_i,
+                                              &eta_sampled);
+                        if (cpdf <= 0.f) {
+                            cont = false;
+                        } else {
+                            alphaTweak = (1.f - (A.gamma * alpha_i)) * alphaTweak;
+                            beta = mul(beta, muls(divs(fc, cpdf), gabs(wic.z)));
+                            float flip = wic.z > 0.f ? 1.f : -1.f;
+                            no = add(is.p, muls(muls(is.gn, SHADOW_BIAS), flip));
+                            nd = to_world(bsdf, wic);
+                            cont = true;
+                        }
+                    } else {
+                        // lower-priority interface: step through (pathintegrator.cpp:223-229)
+                        no = add(is.p, muls(cur.d, SHADOW_BIAS));
+                        nd = cur.d;
+                        flags = F_TRANSMISSIVE;
+                        float bs2 = rng_float(rng);
+                        eta_sampled = bsdf_sample_eta(bsdf, bs2);
+                        cont = true;
+                        have_ed = false;
+                    }
+                    if (cont) {
+                        if (flags & F_TRANSMISSIVE) list.update(is.meshID, is.priority, eta_sampled);
+                        // Russian roulette (pathintegrator.cpp:236-246)
+                        float q = gmax((beta.x + beta.y + beta.z) * 0.33333f, 0.f);
+                        if (bounce > 3) {
+                            if (q >= rng_float(rng)) beta = divs(beta, q);
+                            else cont = false;
+                        }
+                    }
+                    ++bounce;
+                    if (COUNT) n_sh += (use1 ? 1u : 0u) + (use2 ? 1u : 0u);
+                    ext_pending = false;
+                    if (cont && bounce < A.bounces) queue_ext(no, nd);
+                    if (newk) {
+                        waiting = true;
+                    } else {
+                        // no query left (path ended, or ended at the bounce limit): the
+                        // EstimateDirect term of this bounce, if any, is still owed
+                        if (have_ed) L = add(L, mul(muls(F3(0.f, 0.f, 0.f), nL), betak));
+                        done = true;
+                    }
+                } else if (ext_pending) {
+                    // escaped: at bounce 0 the light seen directly is the result (Q6, Q7)
+                    if (bounce == 0 && lightHit) L = Le;
+                }
+                if (done) {
+                    A.Lout[soff + (uint64_t)s * sstr] = make_float4(L.x, L.y, L.z, alpha);
+                    ++s;
+                }
+            }
+        }
+        // pixel refill (persistent grid): one queue atomic per wave
+        if (A.qhead) {
+            const bool need = !waiting && s >= A.spp && slot != 0xFFFFFFFEu;
+            const uint64_t m = __ballot(need);
+            if (m) {
+                const int leader = __builtin_ctzll(m);
+                uint32_t base = 0;
+                if ((int)__lane_id() == leader) base = atomicAdd(A.qhead, (uint32_t)__popcll(m));
+                base = __builtin_amdgcn_readlane(base, leader);
+                if (need) {
+                    const uint32_t idx = A.qbase + base +
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    if (idx < A.n_slots) {
+                        take_pixel(A.queue[idx]);
+                        s = 0;
+                    } else {
+                        slot = 0xFFFFFFFEu;  // queue exhausted: no further refill attempts
+                    }
+                }
+            }
+        }
+        bool active = !waiting && s < A.spp;
+        // new samples (pathintegrator.cpp:144-166; render.cpp:87-95); a zero bounce limit ends a
+        // sample at once, so loop until a ray is queued or the pixel is done
+        while (active) {
+            const float2 sm = A.samples[soff + (uint64_t)s * sstr];
+            const Ray ray = cast_ray(S, F2(sm.x, sm.y), A.W, A.H, px, py);
+            L = F3(0.f, 0.f, 0.f);
+            alpha = 0.f;
+            eta_sampled = 1.f;
+            eta_outer = 1.f;
+            beta = F3(1.f, 1.f, 1.f);
+            flags = 0;
+            alphaTweak = 1.f;
+            bounce = 0;
+            list.n = 0;
+            use1 = use2 = have_ed = false;
+            ext_pending = false;
+            if (A.bounces == 0) {
+                A.Lout[soff + (uint64_t)s * sstr] = make_float4(0.f, 0.f, 0.f, 0.f);
+                ++s;
+                active = s < A.spp;
+                continue;
+            }
+            queue_ext(ray.o, ray.d);
+            waiting = true;
+            active = false;
+        }
+#ifdef NART_WAVEPROF
+        if (COUNT && lane == 0) cnt.pw[11] += __builtin_amdgcn_s_memtime() - prof_tp;  // path phase cycles
+#endif
+        // queued rays: init the result words, then list the (lane, kind) ids in kind order
+        if (newk) {
+            uint4 r0 = *my_res;
+            if (newk & 1u) r0.x = RQ_PENDING;
+            if (newk & 2u) r0.y = 2u;
+            if (newk & 4u) r0.z = 2u;
+            *my_res = r0;
+        }
+        uint32_t nq = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const bool want = (newk >> k) & 1u;
+            const uint64_t m = __ballot(want);
+            if (want) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                s_list[nq + rank] = (uint8_t)(lane | (k << 6));
+            }
+            nq += (uint32_t)__popcll(m);
+        }
+        const bool more = A.qhead && !waiting && s >= A.spp && slot != 0xFFFFFFFEu;  // may still get a pixel
+        if (__ballot(waiting || tracing || more) == 0) break;  // every path of the wave is done
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+
+        // ---------------- traversal phase: lanes take the wave's queued rays in turn
+        uint32_t head = 0;
+#ifdef NART_WAVEPROF
+        const uint64_t prof_tt = __builtin_amdgcn_s_memtime();
+#endif
+        for (;;) {
+            const bool need = !tracing;
+            const uint64_t mn = __ballot(need);
+            if (mn && head < nq) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mn >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)mn, 0u));
+                if (need && head + rank < nq) {
+                    tid8 = s_list[head + rank];
+                    const uint32_t owner = tid8 & 63u, kind = tid8 >> 6;
+                    const float4 a = my_out[(kind * 64 + owner) * 2], b = my_out[(kind * 64 + owner) * 2 + 1];
+                    tr = make_ray(F3(a.x, a.y, a.z), F3(b.x, b.y, b.z));
+                    trav_begin(S, tr, a.w, kind != 0u, tq);
+                    tracing = true;
+                }
+                head += min((uint32_t)__popcll(mn), nq - head);
+            }
+            bool fin = false;
+            if (tracing) {
+                if (COUNT) WPROF(cnt, 0);
+                fin = !S.geometry_visible;  // one-chunk scenes render no geometry (Q14)
+                if (!fin) fin = trav_step<COUNT>(S, tr, tq, sc, nullptr, stride, cnt, s_nodes, nl);
+            }
+            if (fin) {
+                tracing = false;
+                float bt = tq.bestT;
+                uint32_t bg = tq.bestG;
+                if (S.geometry_visible)
+                    oc_resolve<COUNT>(S, tr, tq.tmax, tq.any, tq.risky, tq.bestInfo, fminf(tq.t2, oc_cull(S, tq.bestT)),
+                                      bt, bg, cnt);
+                uint32_t* rw = reinterpret_cast<uint32_t*>(s_res + wv * 64 + (tid8 & 63u));
+                const uint32_t kind = tid8 >> 6;
+                rw[kind] = kind == 0u ? bg : (bg != NO_HIT ? 1u : 0u);
+            }
+            if (head >= nq && (uint32_t)__popcll(__ballot(tracing)) <= A.rq_quorum) break;
+        }
+#ifdef NART_WAVEPROF
+        if (COUNT && (int)__lane_id() == __builtin_ctzll(__ballot(1))) cnt.pw[6] += __builtin_amdgcn_s_memtime() - prof_tt;
+#endif
+    }
+#ifdef NART_WAVEPROF
+    if (COUNT) {
+        if (lane == 0) cnt.pw[7] += __builtin_amdgcn_s_memtime() - prof_t0;
+        for (int i = 0; i < 12; ++i) atomicAdd(&A.counters[8 + i], (unsigned long long)cnt.pw[i]);
+    }
+#endif
     if (COUNT) {
         atomicAdd(&A.counters[0], (unsigned long long)n_ext);
         atomicAdd(&A.counters[1], (unsigned long long)n_sh);

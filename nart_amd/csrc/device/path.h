@@ -75,7 +75,7 @@ struct TraceCounters {
 #ifdef NART_WAVEPROF
     // development profile (counter pass only): wave-level iterations and active lanes of the
     // traversal step / node / triangle loops, cycles in traversal and in total
-    uint64_t pw[10];
+    uint64_t pw[12];
 #endif
 };
 #ifdef NART_WAVEPROF
@@ -142,13 +142,20 @@ ND void trav_begin(const DScene& S, const Ray& r, float tmax, bool ANY, Trav& t)
     t.risky = false;
 }
 
+// Traversal stack entry: one 8-B LDS word (node code, entry distance), so a pop is one
+// ds_read_b64 (sc points at this lane's int2 column, laid out [depth][lane]; st is unused).
+// C3 at 64 spp: 134.3 -> 133.9 ms vs two 4-B arrays.
+ND void stk_push(int* sc, float* st, int stride, int sp, int code, float tn) {
+    reinterpret_cast<int2*>(sc)[sp * stride] = make_int2(code, __float_as_int(tn));
+}
+
 // pop the next subtree that can still contain a closer hit
 ND bool trav_pop(Trav& t, const int* sc, const float* st, int stride) {
     while (t.sp > 0) {
         --t.sp;
-        const float tn = st[t.sp * stride];
-        if (tn <= t.cullT) {
-            t.code = sc[t.sp * stride];
+        const int2 e = reinterpret_cast<const int2*>(sc)[t.sp * stride];
+        if (__int_as_float(e.y) <= t.cullT) {
+            t.code = e.x;
             return true;
         }
     }
@@ -166,6 +173,19 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
         if (COUNT) WPROF(cnt, 2);
         float4 a, b, c;
         int4 k;
+#if defined(NART_LDS_ALL) && defined(__HIP_DEVICE_COMPILE__)
+        // every node staged in LDS (experiment: valid only when the whole BVH fits)
+        if (true) {
+            typedef float v4f __attribute__((ext_vector_type(4)));
+            typedef const __attribute__((address_space(3))) v4f lds_v4f;
+            lds_v4f* np = (lds_v4f*)lnodes + 4 * t.code;
+            const v4f qa = np[0], qb = np[1], qc = np[2], qk = np[3];
+            a = make_float4(qa.x, qa.y, qa.z, qa.w);
+            b = make_float4(qb.x, qb.y, qb.z, qb.w);
+            c = make_float4(qc.x, qc.y, qc.z, qc.w);
+            k = make_int4(__float_as_int(qk.x), __float_as_int(qk.y), __float_as_int(qk.z), __float_as_int(qk.w));
+        } else
+#endif
         if (t.code < nl) {
 #if defined(NART_NODE_DS) && defined(__HIP_DEVICE_COMPILE__)
             // explicit LDS address space: ds_read_b128, not a flat load through the generic aperture
@@ -208,8 +228,7 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
         bool h1 = (n1 <= f1) && (f1 >= 0.f) && (n1 <= t.cullT);
         if (h0 && h1) {
             bool swap = n1 < n0;
-            sc[t.sp * stride] = swap ? k.x : k.y;
-            st[t.sp * stride] = swap ? n0 : n1;
+            stk_push(sc, st, stride, t.sp, swap ? k.x : k.y, swap ? n0 : n1);
             ++t.sp;
             t.code = swap ? k.y : k.x;
         } else if (h0) {
@@ -222,35 +241,30 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
     }
     const uint32_t lc = ~(uint32_t)t.code;
     const uint32_t first = lc >> 5, count = (lc & 31u) + 1u;
-#ifdef NART_TRI_PIPELINE
-    // Software-pipelined leaf: the records of triangle i + 1 are in flight while triangle i is
-    // tested; the last iteration reloads its own record instead of reading past the leaf.
-    // Opt-in: no faster on the C3 full frame.
-    const float4* tp0 = S.tri_isect + 4 * first;
-    float4 na = tp0[0], nb = tp0[1], nc = tp0[2], nd = tp0[3];
-#endif
+    // Vertices pre-permuted for this ray's major axis (DScene::tri_perm): v - o in permuted
+    // order is (vp - op) component by component, the same subtractions as geometry.cpp:42-56,
+    // without 18 per-triangle selects (C3 at 64 spp: 134.9 -> 133.3 ms).  The plane record
+    // {n, dot(v0, n)} is read only for triangles whose edge test passes.
+    const f3 op = permute(r.o, r.major);
+    const float4* tpp = S.tri_perm + 3 * ((size_t)r.major * S.num_leaf_tris + first);
     for (uint32_t i = 0; i < count; ++i) {
         if (COUNT) cnt.tris++;
         if (COUNT) WPROF(cnt, 4);
-#ifdef NART_TRI_PIPELINE
-        const float4 a = na, b = nb, c = nc, dd = nd;
-        {
-            const float4* tq = tp0 + 4 * (i + 1 < count ? i + 1 : i);
-            na = tq[0];
-            nb = tq[1];
-            nc = tq[2];
-            nd = tq[3];
-        }
-#else
-        const float4* tp = S.tri_isect + 4 * (first + i);
-        float4 b = tp[1], c = tp[2], dd = tp[3];
-#endif
-        float e0, e1, e2;
-        edge_functions(r, F3(b.x, b.y, b.z), F3(b.w, c.x, c.y), F3(c.z, c.w, dd.x), e0, e1, e2);
+        const float4 b = tpp[3 * i], c = tpp[3 * i + 1], dd = tpp[3 * i + 2];
+        f3 p0 = F3(b.x - op.x, b.y - op.y, b.z - op.z);
+        f3 p1 = F3(b.w - op.x, c.x - op.y, c.y - op.z);
+        f3 p2 = F3(c.z - op.x, c.w - op.y, dd.x - op.z);
+        p0.x += p0.z * r.Sx;
+        p0.y += p0.z * r.Sy;
+        p1.x += p1.z * r.Sx;
+        p1.y += p1.z * r.Sy;
+        p2.x += p2.z * r.Sx;
+        p2.y += p2.z * r.Sy;
+        const float e0 = (p1.x * p2.y) - (p1.y * p2.x);
+        const float e1 = (p2.x * p0.y) - (p2.y * p0.x);
+        const float e2 = (p0.x * p1.y) - (p0.y * p1.x);
         if (!edges_accept(e0, e1, e2)) continue;
-#ifndef NART_TRI_PIPELINE
-        float4 a = tp[0];
-#endif
+        const float4 a = S.tri_isect[4 * (first + i)];
         f3 n = F3(a.x, a.y, a.z);
         const float den = dot(r.d, n);
         float tt = (a.w - dot(r.o, n)) / den;

@@ -160,7 +160,7 @@ __global__ __launch_bounds__(256) void k_wf_init(DScene S, WFArgs A) {
 template <bool COUNT>
 __global__ __launch_bounds__(256) void k_wf_trace(DScene S, WFArgs A, uint32_t it) {
     extern __shared__ __attribute__((aligned(16))) int s_dyn[];
-    int* sc = s_dyn + threadIdx.x;
+    int* sc = reinterpret_cast<int*>(reinterpret_cast<int2*>(s_dyn) + threadIdx.x);
     float* stn = reinterpret_cast<float*>(s_dyn + A.R.stack_depth * blockDim.x) + threadIdx.x;
     const uint32_t cur = it & 1u, nxt = cur ^ 1u;
     if (blockIdx.x == 0 && threadIdx.x == 0) {

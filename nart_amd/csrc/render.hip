@@ -32,6 +32,7 @@ struct nart_ctx {
     // scene buffers
     void* d_nodes = nullptr;
     void* d_tri_isect = nullptr;
+    void* d_tri_perm = nullptr;
     void* d_tris = nullptr;
     void* d_tri_mesh = nullptr;
     void* d_meshes = nullptr;
@@ -359,9 +360,9 @@ int ensure_queue(nart_ctx* ctx, uint32_t n) {
 
 // LDS of one k_render block: traversal stack + as many top BVH nodes as fit while
 // NART_RENDER_WAVES blocks share a CU's 160 KiB (NART_LDS_NODES overrides the node count).
-uint32_t render_lds_nodes(const nart_ctx* ctx) {
-    const size_t stack = (size_t)ctx->stack_depth * 256 * 8;
-    const size_t budget = (size_t)160 * 1024 / NART_RENDER_WAVES;
+uint32_t render_lds_nodes(const nart_ctx* ctx, size_t fixed = 0, uint32_t blocks_of_256 = 1) {
+    const size_t stack = fixed ? fixed : (size_t)ctx->stack_depth * 256 * 8;
+    const size_t budget = (size_t)160 * 1024 * blocks_of_256 / NART_RENDER_WAVES;
     size_t n = budget > stack ? (budget - stack) / sizeof(BVHNode) : 0;
     if (const char* e = std::getenv("NART_LDS_NODES")) n = (size_t)std::strtoul(e, nullptr, 10);
     return (uint32_t)std::min<size_t>(n, ctx->num_nodes);
@@ -471,12 +472,15 @@ template <int MAXL, bool COUNT, bool ENV>
 int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     auto kern = k_render<MAXL, COUNT, ENV, false>;
     auto kern_q = k_render<MAXL, COUNT, ENV, true>;
+    auto kern_rq = k_render_rq<MAXL, COUNT, ENV>;
     static bool attr = false;  // dynamic LDS above the 64 KiB default
     if (!attr) {
-        for (const void* f : {(const void*)kern, (const void*)kern_q, (const void*)k_render<MAXL, true, ENV, false>})
+        for (const void* f : {(const void*)kern, (const void*)kern_q, (const void*)k_render<MAXL, true, ENV, false>,
+                              (const void*)kern_rq})
             hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
+    const bool rq = ctx->variant == 3;
     // NART_QUORUM_MIN_ROUNDS: rounds of resident waves from which the quorum kernel is used (C3:
     // whole frame 16 rounds 569 -> 517 ms with it, 1/2 frame 8 rounds 332 -> 301, 1/4 4 rounds
     // 183 -> 179, 1/8 2 rounds 108 -> 134)
@@ -485,6 +489,9 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     RenderArgs b = a;
     b.lds_nodes = render_lds_nodes(ctx);
     const size_t lds = (size_t)ctx->stack_depth * 256 * 8 + (size_t)b.lds_nodes * sizeof(BVHNode);
+    RenderArgs brq = a;  // ray-queue kernel: outbox, results and id lists take part of the LDS
+    brq.lds_nodes = render_lds_nodes(ctx, rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK), NART_RQ_BLOCK / 256);
+    const size_t lds_rq = rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK) + (size_t)brq.lds_nodes * sizeof(BVHNode);
     const dim3 block(256);
     uint32_t blocks = (a.n_slots + 255) / 256;
     const int mode = queue_mode();
@@ -495,6 +502,19 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     const uint32_t W = resident * 4;  // resident (persistent) waves
     const double R = (double)a.n_slots / (64.0 * W);  // rounds of resident waves
     if (ctx->variant == 2 || R >= q_rounds) kern = kern_q;
+    // the ray-queue kernel takes kern's place (its own LDS layout); the cost probe keeps k_render
+    auto launch = [&](uint32_t nblocks, const RenderArgs& args) {
+        if (rq) {
+            static const uint32_t rqq = std::getenv("NART_RQ_QUORUM") ? (uint32_t)std::atoi(std::getenv("NART_RQ_QUORUM")) : 8u;
+            RenderArgs r2 = args;
+            r2.lds_nodes = brq.lds_nodes;
+            r2.rq_quorum = rqq;
+            const uint32_t per = NART_RQ_BLOCK / 256;  // launches are counted in blocks of 256
+            hipLaunchKernelGGL(kern_rq, dim3((nblocks + per - 1) / per), dim3(NART_RQ_BLOCK), lds_rq, st, ctx->scene, r2);
+        } else {
+            hipLaunchKernelGGL(kern, dim3(nblocks), block, lds, st, ctx->scene, args);
+        }
+    };
     if (mode > 0) {
         if (blocks > resident) {  // more pixels than resident lanes: persistent grid + queue
             const uint32_t n = a.n_slots;
@@ -507,7 +527,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             if (R >= 12.0 && mode == 2 && !std::getenv("NART_QUEUE_K")) {
                 // many rounds: the slot order (costly waves interleaved with cheap ones in time)
                 // measured faster than any reordering; no probe
-                hipLaunchKernelGGL(kern, dim3(blocks), block, lds, st, ctx->scene, b);
+                launch(blocks, b);
                 HIPCHK(hipGetLastError());
                 return NART_OK;
             }
@@ -525,7 +545,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                 size_t tmp = 0;
                 if (k == 64u) {  // whole groups, costliest first (coherent waves, longest chains first)
                     b.queue = ctx->d_queue;
-                    hipLaunchKernelGGL(kern, dim3(blocks), block, lds, st, ctx->scene, b);
+                    launch(blocks, b);
                     HIPCHK(hipGetLastError());
                     return NART_OK;
                 }
@@ -548,7 +568,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             }
         }
     }
-    hipLaunchKernelGGL(kern, dim3(blocks), block, lds, st, ctx->scene, b);
+    launch(blocks, b);
     HIPCHK(hipGetLastError());
     return NART_OK;
 }
@@ -975,8 +995,8 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
                     fclose(f);
                 }
             }
-            fprintf(stderr, "WAVEPROF steps %llu/%llu nodes %llu/%llu tris %llu/%llu trav_cyc %llu total_cyc %llu shade %llu/%llu\n",
-                    w[8], w[9], w[10], w[11], w[12], w[13], w[14], w[15], w[16], w[17]);
+            fprintf(stderr, "WAVEPROF steps %llu/%llu nodes %llu/%llu tris %llu/%llu trav_cyc %llu total_cyc %llu shade %llu/%llu phases %llu path_cyc %llu\n",
+                    w[8], w[9], w[10], w[11], w[12], w[13], w[14], w[15], w[16], w[17], w[18], w[19]);
 #endif
         }
     }
@@ -993,7 +1013,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     if (!ctx) return NART_E_OOM;
     *out = nullptr;
     ctx->device = device_id;
-    if (const char* v = std::getenv("NART_VARIANT")) ctx->variant = std::max(0, std::min(2, std::atoi(v)));
+    if (const char* v = std::getenv("NART_VARIANT")) ctx->variant = std::max(0, std::min(3, std::atoi(v)));
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device_id || device_id < 0) {
         delete ctx;
@@ -1040,6 +1060,28 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     if ((rc = upload(ctx, ctx->d_nodes, bvh.nodes.data(), bvh.nodes.size()))) return bail(rc);
     ctx->num_nodes = (uint32_t)bvh.nodes.size();
     if ((rc = upload(ctx, ctx->d_tri_isect, bvh.tri_isect.data(), bvh.tri_isect.size()))) return bail(rc);
+    {
+        // vertex block of every triangle test record, permuted for each ray major axis
+        const size_t nt = bvh.tri_isect.size() / 16;
+        std::vector<float> perm(3 * nt * 12);
+        for (int m = 0; m < 3; ++m) {
+            const int kx = (m + 1) % 3, ky = (m + 2) % 3, kz = m;
+            for (size_t i = 0; i < nt; ++i) {
+                const float* r = &bvh.tri_isect[i * 16];
+                const float* v[3] = {r + 4, r + 7, r + 10};  // v0, v1, v2 (words 4-12)
+                float* o = &perm[((size_t)m * nt + i) * 12];
+                for (int k = 0; k < 3; ++k) {
+                    o[3 * k + 0] = v[k][kx];
+                    o[3 * k + 1] = v[k][ky];
+                    o[3 * k + 2] = v[k][kz];
+                }
+                o[9] = r[13];   // global index
+                o[10] = r[14];  // octree leaf | inside bit
+                o[11] = r[15];  // grazing threshold
+            }
+        }
+        if ((rc = upload(ctx, ctx->d_tri_perm, perm.data(), perm.size()))) return bail(rc);
+    }
     if ((rc = upload(ctx, ctx->d_tris, blob->triangles, blob->num_triangles))) return bail(rc);
     std::vector<uint32_t> tri_mesh(blob->num_triangles);
     std::vector<DMesh> meshes(blob->num_meshes);
@@ -1098,6 +1140,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     std::memset(&S, 0, sizeof(S));
     S.nodes = (const BVHNode*)ctx->d_nodes;
     S.tri_isect = (const float4*)ctx->d_tri_isect;
+    S.tri_perm = (const float4*)ctx->d_tri_perm;
     S.tris = (const nart_triangle*)ctx->d_tris;
     S.tri_mesh = (const uint32_t*)ctx->d_tri_mesh;
     S.meshes = (const DMesh*)ctx->d_meshes;
@@ -1109,6 +1152,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     if ((rc = build_medium(ctx, blob->medium, S.medium))) return bail(rc);
     S.num_lights = blob->num_lights;
     S.num_tris = blob->num_triangles;
+    S.num_leaf_tris = (uint32_t)(bvh.tri_isect.size() / 16);
     S.root = bvh.root_code;
     S.geometry_visible = (!root_leaf && bvh.num_leaf_tris > 0) ? 1 : 0;
     std::memcpy(S.cam_m, blob->camera.m, sizeof(S.cam_m));
@@ -1143,7 +1187,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
 void nart_hip_destroy(nart_ctx* ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
-    void* bufs[] = {ctx->d_nodes, ctx->d_tri_isect, ctx->d_tris, ctx->d_tri_mesh, ctx->d_meshes, ctx->d_mats,
+    void* bufs[] = {ctx->d_nodes, ctx->d_tri_isect, ctx->d_tri_perm, ctx->d_tris, ctx->d_tri_mesh, ctx->d_meshes, ctx->d_mats,
                     ctx->d_lights, ctx->d_texs, ctx->d_tex_pool, ctx->d_slot_xy, ctx->d_slot_so, ctx->d_rng, ctx->d_samples,
                     ctx->d_L, ctx->d_bucket_ids, ctx->d_bucket_base, ctx->d_table, ctx->d_counters, ctx->d_wf, ctx->d_envs, ctx->d_density,
                     ctx->d_oc_nodes, ctx->d_oc_chunks, ctx->d_oc_tris, ctx->d_tri_leaf, ctx->d_oc_lock, ctx->d_oc_heap,
@@ -1171,8 +1215,9 @@ int nart_hip_set_counters(nart_ctx* ctx, int enable) {
 
 int nart_hip_set_variant(nart_ctx* ctx, int variant) {
     if (!ctx) return NART_E_INVALID;
-    if (variant < 0 || variant > 2)
-        return fail(ctx, NART_E_UNSUPPORTED, "variant must be 0 (megakernel), 1 (wavefront) or 2 (megakernel, quorum always)");
+    if (variant < 0 || variant > 3)
+        return fail(ctx, NART_E_UNSUPPORTED, "variant must be 0 (megakernel), 1 (wavefront), 2 (megakernel, quorum "
+                                             "always) or 3 (megakernel with a wave ray queue)");
     ctx->variant = variant;
     return NART_OK;
 }

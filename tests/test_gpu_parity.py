@@ -31,10 +31,11 @@ def _report(a, b):
     return "%d of %d floats differ, max abs diff %g" % (int(ne.sum()), ne.size, float(np.nanmax(np.abs(a - b))))
 
 
-VARIANTS = [0, 1, 2]  # megakernel, wavefront, megakernel with the traversal quorum forced on
+VARIANTS = [0, 1, 2, 3]  # megakernel, wavefront, megakernel with the traversal quorum forced on, wave ray queue
+VARIANT_IDS = ["megakernel", "wavefront", "quorum", "rayqueue"]
 
 
-@pytest.fixture(scope="module", params=VARIANTS, ids=["megakernel", "wavefront", "quorum"])
+@pytest.fixture(scope="module", params=VARIANTS, ids=VARIANT_IDS)
 def glass_gpu(request, gpu, glass_scene):
     return nart_amd.HipRenderer(glass_scene, variant=request.param)
 
@@ -114,7 +115,7 @@ def test_framebuffer_ragged_buckets(glass_gpu, glass_oracle, glass_scene):
     assert _bits_equal(g, r), _report(g, r)
 
 
-@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("variant", VARIANTS, ids=VARIANT_IDS)
 def test_cornell_box(gpu, cornell_scene, variant):
     p = _params(cornell_scene, 96, 64, 8)
     g = nart_amd.HipRenderer(cornell_scene, variant=variant).render(p)
@@ -122,7 +123,7 @@ def test_cornell_box(gpu, cornell_scene, variant):
     assert _bits_equal(g, r), _report(g, r)
 
 
-@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("variant", VARIANTS, ids=VARIANT_IDS)
 def test_materials_scene(gpu, materials_scene, variant):
     """All five material types, textured rho_d / roughness / normal maps (EXR via the ZIP reader),
     ring + disk lights, nested dielectrics with priorities (scenes.materials)."""
@@ -139,7 +140,7 @@ def test_materials_per_sample(gpu, materials_scene):
     assert _bits_equal(g, r), _report(g, r)
 
 
-@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("variant", VARIANTS, ids=VARIANT_IDS)
 @pytest.mark.parametrize("which", ["textured", "constant"])
 def test_environment_light(gpu, env_scene, env_const_scene, variant, which):
     """Environment light (environmentlight.cpp:9-79): lat-long Li via the glibc acosf/atan2f
@@ -189,7 +190,7 @@ def test_volume_per_sample(gpu, volume_scenes):
     assert _bits_equal(g, r), _report(g, r)
 
 
-@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("variant", VARIANTS, ids=VARIANT_IDS)
 @pytest.mark.parametrize("name", ["ring", "veach"])
 def test_reference_scenes_all_sessions(gpu, ref_scenes, name, variant):
     """The reference's own ring.json (every session: roughening 0 / 0.2 / 0.3) and veach.json
@@ -251,7 +252,7 @@ def test_bucket_api_matches_render(gpu, glass_gpu, glass_scene):
 C2_OCTREE_BUCKETS = [1356, 1403, 1476, 1700, 1820, 2676, 3203, 4020, 4121, 5083, 5196, 6922, 7286, 7820, 8106]
 
 
-@pytest.mark.parametrize("variant", VARIANTS, ids=["megakernel", "wavefront", "quorum"])
+@pytest.mark.parametrize("variant", VARIANTS, ids=VARIANT_IDS)
 def test_octree_boundary_rejections(gpu, cornell_scene, variant):
     import torch
     p = _params(cornell_scene, 1920, 1080, 64)
