@@ -213,7 +213,7 @@ def main():
                 "measured_frac": (round(traffic / (kernel_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
                                   if traffic else None),
                 "traffic_source": traffic_src,
-                "kernel": "k_render_volume_sm" if p.integrator == 1 else "k_render",
+                "kernel": "k_render_volume_sm" if p.integrator == 1 else "k_render_rq",
                 "kernel_avg_ms": round(kernel_avg_ms, 3), "bytes_per_sample": round(bps, 1)}
     if rank == 0:
         img_ok = bool(torch.isfinite(image).all().item())

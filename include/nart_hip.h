@@ -96,9 +96,12 @@ typedef struct nart_bvh_info {
 } nart_bvh_info;
 int nart_hip_bvh_info(const nart_scene_blob* scene, nart_bvh_info* out);
 
-/* Kernel variant: 0 = megakernel (one lane per pixel slot; traversal quorum on when the launch
-   spans >= 3 rounds of resident waves), 1 = wavefront (ray queues), 2 = megakernel with the
-   traversal quorum on for every launch (parity tests of that path at small sizes). */
+/* Kernel variant (all render bit-identical images):
+   0 = megakernel with a wave ray queue (default; one lane per pixel slot, the lanes of a wave
+       trace each other's queued shadow and continuation rays),
+   1 = wavefront (ray queues in HBM),
+   2 = megakernel with the traversal quorum on for every launch (parity tests at small sizes),
+   3 = megakernel, traversal quorum on when the launch spans >= 3 rounds of resident waves. */
 int nart_hip_set_variant(nart_ctx* ctx, int variant);
 
 #ifdef __cplusplus

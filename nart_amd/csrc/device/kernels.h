@@ -758,6 +758,17 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
 
 #ifdef NART_WAVEPROF
     const uint64_t prof_t0 = __builtin_amdgcn_s_memtime();
+    uint64_t prof_sec[4] = {0, 0, 0, 0};  // path phase: results + shading, refill, new samples, id lists
+    uint64_t prof_last = prof_t0;
+    uint32_t prof_shn = 0, prof_sht = 0;  // node visits / triangle tests of shadow rays
+#define RQ_MARK(i)                                                 \
+    do {                                                           \
+        const uint64_t _n = __builtin_amdgcn_s_memtime();          \
+        prof_sec[i] += _n - prof_last;                             \
+        prof_last = _n;                                            \
+    } while (0)
+#else
+#define RQ_MARK(i) ((void)0)
 #endif
     auto put_ray = [&](int kind, f3 o, f3 d, float tmax) {
         float4* e = my_out + (kind * 64 + lane) * 2;
@@ -792,6 +803,7 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
 #ifdef NART_WAVEPROF
         if (COUNT && lane == 0) cnt.pw[10]++;  // path phases
         const uint64_t prof_tp = __builtin_amdgcn_s_memtime();
+        prof_last = prof_tp;
 #endif
         if (waiting) {
             const uint4 r = *my_res;
@@ -931,6 +943,7 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                 }
             }
         }
+        RQ_MARK(0);
         // pixel refill (persistent grid): one queue atomic per wave
         if (A.qhead) {
             const bool need = !waiting && s >= A.spp && slot != 0xFFFFFFFEu;
@@ -953,6 +966,7 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
             }
         }
         bool active = !waiting && s < A.spp;
+        RQ_MARK(1);
         // new samples (pathintegrator.cpp:144-166; render.cpp:87-95); a zero bounce limit ends a
         // sample at once, so loop until a ray is queued or the pixel is done
         while (active) {
@@ -979,6 +993,7 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
             waiting = true;
             active = false;
         }
+        RQ_MARK(2);
 #ifdef NART_WAVEPROF
         if (COUNT && lane == 0) cnt.pw[11] += __builtin_amdgcn_s_memtime() - prof_tp;  // path phase cycles
 #endif
@@ -1002,6 +1017,7 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
             }
             nq += (uint32_t)__popcll(m);
         }
+        RQ_MARK(3);
         const bool more = A.qhead && !waiting && s >= A.spp && slot != 0xFFFFFFFEu;  // may still get a pixel
         if (__ballot(waiting || tracing || more) == 0) break;  // every path of the wave is done
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1031,7 +1047,13 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
             if (tracing) {
                 if (COUNT) WPROF(cnt, 0);
                 fin = !S.geometry_visible;  // one-chunk scenes render no geometry (Q14)
+#ifdef NART_WAVEPROF
+                const uint32_t pn0 = cnt.nodes, pt0 = cnt.tris;
+#endif
                 if (!fin) fin = trav_step<COUNT>(S, tr, tq, sc, nullptr, stride, cnt, s_nodes, nl);
+#ifdef NART_WAVEPROF
+                if (COUNT && (tid8 >> 6) != 0u) { prof_shn += cnt.nodes - pn0; prof_sht += cnt.tris - pt0; }
+#endif
             }
             if (fin) {
                 tracing = false;
@@ -1054,8 +1076,13 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
     if (COUNT) {
         if (lane == 0) cnt.pw[7] += __builtin_amdgcn_s_memtime() - prof_t0;
         for (int i = 0; i < 12; ++i) atomicAdd(&A.counters[8 + i], (unsigned long long)cnt.pw[i]);
+        if (lane == 0)
+            for (int i = 0; i < 4; ++i) atomicAdd(&A.counters[24 + 8 * 69999 + i], (unsigned long long)prof_sec[i]);
+        atomicAdd(&A.counters[24 + 8 * 69999 + 4], (unsigned long long)prof_shn);
+        atomicAdd(&A.counters[24 + 8 * 69999 + 5], (unsigned long long)prof_sht);
     }
 #endif
+#undef RQ_MARK
     if (COUNT) {
         atomicAdd(&A.counters[0], (unsigned long long)n_ext);
         atomicAdd(&A.counters[1], (unsigned long long)n_sh);

@@ -480,7 +480,9 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
-    const bool rq = ctx->variant == 3;
+    // variant 0: ray-queue kernel; 2: k_render with the traversal quorum on every launch;
+    // 3: k_render with the quorum chosen by rounds of resident waves (the previous default)
+    const bool rq = ctx->variant == 0;
     // NART_QUORUM_MIN_ROUNDS: rounds of resident waves from which the quorum kernel is used (C3:
     // whole frame 16 rounds 569 -> 517 ms with it, 1/2 frame 8 rounds 332 -> 301, 1/4 4 rounds
     // 183 -> 179, 1/8 2 rounds 108 -> 134)
@@ -995,6 +997,12 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
                     fclose(f);
                 }
             }
+            {
+                unsigned long long sc[8];
+                HIPCHK(hipMemcpy(sc, ctx->d_counters + 24 + 8 * 69999, sizeof(sc), hipMemcpyDeviceToHost));
+                fprintf(stderr, "WAVEPROF rq path sections results+shading %llu refill %llu new_samples %llu id_lists %llu shadow nodes %llu tris %llu\n",
+                        sc[0], sc[1], sc[2], sc[3], sc[4], sc[5]);
+            }
             fprintf(stderr, "WAVEPROF steps %llu/%llu nodes %llu/%llu tris %llu/%llu trav_cyc %llu total_cyc %llu shade %llu/%llu phases %llu path_cyc %llu\n",
                     w[8], w[9], w[10], w[11], w[12], w[13], w[14], w[15], w[16], w[17], w[18], w[19]);
 #endif
@@ -1216,8 +1224,8 @@ int nart_hip_set_counters(nart_ctx* ctx, int enable) {
 int nart_hip_set_variant(nart_ctx* ctx, int variant) {
     if (!ctx) return NART_E_INVALID;
     if (variant < 0 || variant > 3)
-        return fail(ctx, NART_E_UNSUPPORTED, "variant must be 0 (megakernel), 1 (wavefront), 2 (megakernel, quorum "
-                                             "always) or 3 (megakernel with a wave ray queue)");
+        return fail(ctx, NART_E_UNSUPPORTED, "variant must be 0 (megakernel with a wave ray queue), 1 (wavefront), 2 "
+                                             "(megakernel, traversal quorum always) or 3 (megakernel, quorum by rounds)");
     ctx->variant = variant;
     return NART_OK;
 }

@@ -31,8 +31,10 @@ def _report(a, b):
     return "%d of %d floats differ, max abs diff %g" % (int(ne.sum()), ne.size, float(np.nanmax(np.abs(a - b))))
 
 
-VARIANTS = [0, 1, 2, 3]  # megakernel, wavefront, megakernel with the traversal quorum forced on, wave ray queue
-VARIANT_IDS = ["megakernel", "wavefront", "quorum", "rayqueue"]
+# ray-queue megakernel (default), wavefront, megakernel with the traversal quorum forced on,
+# megakernel with the quorum chosen by rounds of resident waves
+VARIANTS = [0, 1, 2, 3]
+VARIANT_IDS = ["rayqueue", "wavefront", "quorum", "megakernel"]
 
 
 @pytest.fixture(scope="module", params=VARIANTS, ids=VARIANT_IDS)

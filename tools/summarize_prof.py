@@ -46,13 +46,13 @@ def main(src, tag, config="1920x1080x256"):
                              "duration_ms_fetch_pass": f[1], "duration_ms_write_pass": w[1],
                              "vgpr_count": d["vgpr"], "sgpr_count": d["sgpr"], "lds_bytes": d["lds"],
                              "scratch_bytes": d["scratch"]}
-    def timed_render(name):  # k_render<MAXL, COUNT, ENV, QR>: not the counter / cost-probe pass
-        if "k_render<" not in name:
+    def timed_render(name):  # k_render_rq<MAXL, COUNT, ENV> / k_render<...>: not the counter / cost-probe pass
+        if "k_render_rq<" not in name and "k_render<" not in name:
             return False
         args = [a.strip() for a in name.split("<", 1)[1].split(">", 1)[0].split(",")]
         return len(args) >= 2 and args[1] == "false"
 
-    render = [k for k in out["kernels"] if timed_render(k)]
+    render = sorted((k for k in out["kernels"] if timed_render(k)), key=lambda k: "k_render_rq<" not in k)
     if render:
         r = out["kernels"][render[0]]
         out["hbm_bytes_per_launch"] = r["fetch_bytes"] + r["write_bytes"]
