@@ -42,6 +42,8 @@ typedef struct nart_render_stats {
     /* Counter pass only: hits whose octree reachability needed the exact ancestor-chain check,
      * and queries answered by replaying the reference octree search (device/octree.h). */
     uint64_t octree_checks, octree_replays;
+    double primary_ms;      /* part of kernel_ms: the camera-ray kernel that runs before the path
+                               kernel (k_primary, default variant only)                  */
 } nart_render_stats;
 
 /* Upload the scene, build the device BVH.  device_id: HIP ordinal. */
@@ -103,6 +105,13 @@ int nart_hip_bvh_info(const nart_scene_blob* scene, nart_bvh_info* out);
    2 = megakernel with the traversal quorum on for every launch (parity tests at small sizes),
    3 = megakernel, traversal quorum on when the launch spans >= 3 rounds of resident waves. */
 int nart_hip_set_variant(nart_ctx* ctx, int variant);
+
+/* Splat kernel (all bit-identical): 3 = four tile pixels per lane (default); 4 = one bucket per
+   block, samples staged through LDS by source-row chunks; 2, 1, 0 = one tile pixel per lane
+   with the compare-only / threshold / direct filter-index arithmetic.  Modes fall back to the
+   next lower one where their preconditions (power-of-two buckets, threshold table, LDS size)
+   do not hold. */
+int nart_hip_set_splat_mode(nart_ctx* ctx, int mode);
 
 #ifdef __cplusplus
 }

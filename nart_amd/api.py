@@ -64,7 +64,7 @@ class RenderStats(ctypes.Structure):
                 ("traced_samples", ctypes.c_uint64), ("rays_extend", ctypes.c_uint64), ("rays_shadow", ctypes.c_uint64),
                 ("node_visits", ctypes.c_uint64), ("tri_tests", ctypes.c_uint64), ("bounces", ctypes.c_uint64),
                 ("latin_ms", ctypes.c_double), ("octree_checks", ctypes.c_uint64),
-                ("octree_replays", ctypes.c_uint64)]
+                ("octree_replays", ctypes.c_uint64), ("primary_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
@@ -103,6 +103,7 @@ _HIP_SIGS = {
     "nart_hip_set_counters": (ctypes.c_int, [_P, ctypes.c_int]),
     "nart_hip_eval_sincos": (ctypes.c_int, [_P, _P, ctypes.c_uint32, _P, _P]),
     "nart_hip_set_variant": (ctypes.c_int, [_P, ctypes.c_int]),
+    "nart_hip_set_splat_mode": (ctypes.c_int, [_P, ctypes.c_int]),
     "nart_hip_splat_thresholds": (ctypes.c_int, [ctypes.c_float, _P]),
     "nart_hip_bvh_info": (ctypes.c_int, [_P, ctypes.POINTER(BvhInfo)]),
 }
@@ -255,7 +256,7 @@ class Scene:
 class HipRenderer:
     """nart_ctx: the scene resident on one GPU; Render()-equivalent entry points."""
 
-    def __init__(self, scene, device=0, variant=None):
+    def __init__(self, scene, device=0, variant=None, splat_mode=None):
         self._lib = hip_lib()
         self.scene = scene
         self.device = device
@@ -265,10 +266,18 @@ class HipRenderer:
             raise NartError(rc, "nart_hip_create failed on device %d" % device)
         if variant is not None:
             self.set_variant(variant)
+        if splat_mode is not None:
+            self.set_splat_mode(splat_mode)
 
     def set_variant(self, variant):
-        """0 = megakernel, 1 = wavefront (trace/shade over ray queues); identical results."""
+        """0 = megakernel with a wave ray queue (default), 1 = wavefront (trace/shade over ray
+        queues), 2 / 3 = megakernel with the traversal quorum always / by rounds; identical results."""
         self._check(self._lib.nart_hip_set_variant(self._ctx, int(variant)))
+
+    def set_splat_mode(self, mode):
+        """3 = four pixels per lane (default), 4 = LDS-staged bucket splat, 2-0 = one pixel per
+        lane (include/nart_hip.h); identical results."""
+        self._check(self._lib.nart_hip_set_splat_mode(self._ctx, int(mode)))
 
     def _check(self, rc):
         if rc != NART_OK:

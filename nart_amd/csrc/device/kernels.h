@@ -104,6 +104,7 @@ struct RenderArgs {
     uint32_t* cost = nullptr; // cost probe: per-slot work estimate of the rendered sample(s)
     uint32_t rq_quorum = 8;   // k_render_rq: leave a traversal phase once the wave's queue is empty
                               // and at most this many lanes still trace
+    const uint32_t* prim = nullptr;  // k_render_rq: camera-ray hits from k_primary, same indexing as samples
 };
 
 ND size_t sample_index(const RenderArgs& A, uint32_t slot, uint32_t s) {
@@ -676,6 +677,47 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
     }
 }
 
+// ---------------------------------------------------------------- camera rays, traced coherently
+// The closest hit of every sample's camera ray depends only on its LatinSquare sample, not on the
+// RNG stream, so all of a batch's camera rays are traced here before the path kernel runs: lane =
+// traced pixel, all lanes of a wave (a 16x4 block of a bucket) on the same sample index at once,
+// so their rays run nearly the same traversal (the path kernel's lanes are at unrelated path
+// stages).  Light loop bound (pathintegrator.cpp:167-182) and octree answer as in k_render_rq;
+// hit[sample] = closest triangle or NO_HIT.
+template <bool COUNT, bool ENV>
+__global__ __launch_bounds__(256) void k_primary(DScene S, RenderArgs A, uint32_t* hit) {
+    extern __shared__ __attribute__((aligned(16))) int s_dyn[];
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot >= A.n_slots) return;
+    int* sc = reinterpret_cast<int*>(reinterpret_cast<int2*>(s_dyn) + threadIdx.x);
+    const uint32_t xy = A.slot_xy[slot];
+    const uint32_t px = xy & 0xFFFFu, py = xy >> 16;
+    const SlotSO so = A.slot_so[slot];
+    TraceCounters cnt = {0u, 0u, 0u, 0u};
+    for (uint32_t s = 0; s < A.spp; ++s) {
+        const uint64_t idx = so.first + (uint64_t)s * so.stride;
+        const float2 sm = A.samples[idx];
+        const Ray ray = cast_ray(S, F2(sm.x, sm.y), A.W, A.H, px, py);
+        float lightTMax = __builtin_inff();
+        for (uint32_t j = 0; j < S.num_lights; ++j) {
+            float lt = __builtin_inff();
+            light_li<ENV>(S, S.lights[j], ray.o, ray.d, nullptr, lt);
+            if (lt < lightTMax) lightTMax = lt;
+        }
+        float bt;
+        uint32_t bg;
+        traverse<COUNT>(S, ray, lightTMax, false, bt, bg, sc, nullptr, blockDim.x, cnt, nullptr, 0);
+        hit[idx] = bg;
+    }
+    if (COUNT) {
+        atomicAdd(&A.counters[0], (unsigned long long)A.spp);
+        atomicAdd(&A.counters[2], (unsigned long long)cnt.nodes);
+        atomicAdd(&A.counters[3], (unsigned long long)cnt.tris);
+        atomicAdd(&A.counters[5], (unsigned long long)cnt.oc_checks);
+        atomicAdd(&A.counters[6], (unsigned long long)cnt.oc_replays);
+    }
+}
+
 // ---------------------------------------------------------------- path tracing with a wave ray queue
 // k_render_rq: the same per-lane path state machine as k_render (one lane per traced pixel,
 // its samples in order on one RNG stream), but the lanes of a wave share their rays.  Shading
@@ -776,8 +818,9 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
         e[1] = make_float4(d.x, d.y, d.z, 0.f);
         newk |= 1u << kind;
     };
-    // light intersections of a new extension ray (pathintegrator.cpp:167-182), then queue it
-    auto queue_ext = [&](f3 o, f3 d) {
+    // light intersections of a new extension ray (pathintegrator.cpp:167-182): Le, lightHit,
+    // alpha; returns the query bound
+    auto light_loop = [&](f3 o, f3 d) {
         float lightTMax = __builtin_inff();
         lightHit = false;
         Le = F3(0.f, 0.f, 0.f);
@@ -791,7 +834,10 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                 alpha = 1.f;
             }
         }
-        put_ray(0, o, d, lightTMax);
+        return lightTMax;
+    };
+    auto queue_ext = [&](f3 o, f3 d) {
+        put_ray(0, o, d, light_loop(o, d));
         ext_pending = true;
         if (COUNT) ++n_ext;
     };
@@ -805,6 +851,10 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
         const uint64_t prof_tp = __builtin_amdgcn_s_memtime();
         prof_last = prof_tp;
 #endif
+        // 1. results of lanes whose queries are all in: EstimateDirect term, then the hit to
+        //    shade or the end of the sample
+        bool need_shade = false;
+        uint32_t hitg = NO_HIT;
         if (waiting) {
             const uint4 r = *my_res;
             if ((!ext_pending || r.x != RQ_PENDING) && (!use1 || r.y != 2u) && (!use2 || r.z != 2u)) {
@@ -816,128 +866,12 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                     if (use2 && r.z == 0u) Led = add(Led, c2);
                     L = add(L, mul(muls(Led, nL), betak));
                 }
-                bool done = true;
                 if (ext_pending && r.x != NO_HIT) {
-                    // ---- shade the hit (pathintegrator.cpp:185-246)
-                    done = false;
-                    if (COUNT) ++n_bounce;
-                    if (COUNT) WPROF(cnt, 8);
-                    const float4 ro = my_out[lane * 2], rd = my_out[lane * 2 + 1];
-                    const Ray cur = make_ray(F3(ro.x, ro.y, ro.z), F3(rd.x, rd.y, rd.z));
-                    Isect is;
-                    fill_isect(S, cur, r.x, is);
-                    BSDF bsdf;
-                    create_bsdf(S, is, alphaTweak, bsdf);
-                    use1 = use2 = false;
-                    bool cont;
-                    f3 no, nd;
-                    if (list.valid(is.meshID, is.priority, eta_outer)) {
-                        if (bounce == 0) alpha = 1.f;
-                        const f3 wo = to_local(bsdf, neg(cur.d));
-                        // ---- EstimateDirect (pathintegrator.cpp:38-121)
-                        const DLight& Lg = S.lights[f2u8(gmin(rng_float(rng), ND_ONE_MINUS_EPS) * nL)];
-                        float sPdf = 0.f, lPdf = 0.f;
-                        float sx = rng_float(rng);
-                        float sy = rng_float(rng);
-                        float bsmp = rng_float(rng);
-                        uint32_t dflags = 0;
-                        f3 wi;
-                        f3 f = bsdf_sample_f(bsdf, wo, wi, bsmp, F2(sx, sy), sPdf, dflags, true, eta_outer, nullptr,
-                                             nullptr);
-                        if (sPdf > 0.f) {
-                            float flip = wi.z > 0.f ? 1.f : -1.f;
-                            f3 wW = to_world(bsdf, wi);
-                            float lt = __builtin_inff();
-                            f3 Li = light_li<ENV>(S, Lg, is.p, wW, &lPdf, lt);
-                            float weight = 1.f;
-                            bool add1 = true;
-                            if (!(dflags & F_SPECULAR)) {
-                                weight = (sPdf * sPdf) / (sPdf * sPdf + lPdf * lPdf);
-                                add1 = lPdf > 0.f;
-                            }
-                            if (add1) {
-                                c1 = divs(muls(muls(mul(f, Li), gabs(wi.z)), weight), sPdf);
-                                // an all-zero term cannot change the sum: skip its shadow ray
-                                use1 = !(c1.x == 0.f && c1.y == 0.f && c1.z == 0.f);
-                                if (use1) put_ray(1, add(is.p, muls(muls(is.gn, SHADOW_BIAS), flip)), wW, lt);
-                            }
-                        }
-                        lPdf = 0.f;
-                        float lx = rng_float(rng);
-                        float ly = rng_float(rng);
-                        f3 wiW;
-                        float lt2 = __builtin_inff();
-                        f3 Li2 = light_sample_li<ENV>(S, Lg, is.p, wiW, F2(lx, ly), lPdf, lt2);
-                        f3 wi2 = to_local(bsdf, wiW);
-                        if (lPdf > 0.f) {
-                            float sp2 = bsdf_pdf(bsdf, wo, wi2, true, eta_outer);
-                            if (sp2 > 0.f) {
-                                f3 fv = bsdf_f(bsdf, wo, wi2, true, eta_outer);
-                                float weight = (lPdf * lPdf) / (sp2 * sp2 + lPdf * lPdf);
-                                c2 = divs(muls(muls(mul(fv, Li2), gabs(wi2.z)), weight), lPdf);
-                                use2 = !(c2.x == 0.f && c2.y == 0.f && c2.z == 0.f);
-                                if (use2) {
-                                    float flip2 = wi2.z > 0.f ? 1.f : -1.f;
-                                    put_ray(2, add(is.p, muls(muls(is.gn, SHADOW_BIAS), flip2)), wiW, lt2);
-                                }
-                            }
-                        }
-                        betak = beta;
-                        have_ed = true;
-                        // ---- continuation (pathintegrator.cpp:199-220)
-                        float a = rng_float(rng);
-                        float b = rng_float(rng);
-                        float bs2 = rng_float(rng);
-                        float cpdf = 0.f, alpha_i = 0.f;
-                        f3 wic;
-                        f3 fc = bsdf_sample_f(bsdf, wo, wic, bs2, F2(a, b), cpdf, flags, false, eta_outer, &alpha_i,
-                                              &eta_sampled);
-                        if (cpdf <= 0.f) {
-                            cont = false;
-                        } else {
-                            alphaTweak = (1.f - (A.gamma * alpha_i)) * alphaTweak;
-                            beta = mul(beta, muls(divs(fc, cpdf), gabs(wic.z)));
-                            float flip = wic.z > 0.f ? 1.f : -1.f;
-                            no = add(is.p, muls(muls(is.gn, SHADOW_BIAS), flip));
-                            nd = to_world(bsdf, wic);
-                            cont = true;
-                        }
-                    } else {
-                        // lower-priority interface: step through (pathintegrator.cpp:223-229)
-                        no = add(is.p, muls(cur.d, SHADOW_BIAS));
-                        nd = cur.d;
-                        flags = F_TRANSMISSIVE;
-                        float bs2 = rng_float(rng);
-                        eta_sampled = bsdf_sample_eta(bsdf, bs2);
-                        cont = true;
-                        have_ed = false;
-                    }
-                    if (cont) {
-                        if (flags & F_TRANSMISSIVE) list.update(is.meshID, is.priority, eta_sampled);
-                        // Russian roulette (pathintegrator.cpp:236-246)
-                        float q = gmax((beta.x + beta.y + beta.z) * 0.33333f, 0.f);
-                        if (bounce > 3) {
-                            if (q >= rng_float(rng)) beta = divs(beta, q);
-                            else cont = false;
-                        }
-                    }
-                    ++bounce;
-                    if (COUNT) n_sh += (use1 ? 1u : 0u) + (use2 ? 1u : 0u);
-                    ext_pending = false;
-                    if (cont && bounce < A.bounces) queue_ext(no, nd);
-                    if (newk) {
-                        waiting = true;
-                    } else {
-                        // no query left (path ended, or ended at the bounce limit): the
-                        // EstimateDirect term of this bounce, if any, is still owed
-                        if (have_ed) L = add(L, mul(muls(F3(0.f, 0.f, 0.f), nL), betak));
-                        done = true;
-                    }
-                } else if (ext_pending) {
-                    // escaped: at bounce 0 the light seen directly is the result (Q6, Q7)
-                    if (bounce == 0 && lightHit) L = Le;
-                }
-                if (done) {
+                    need_shade = true;
+                    hitg = r.x;
+                } else {
+                    // escaped (at bounce 0 the light seen directly is the result, Q6, Q7) or ended
+                    if (ext_pending && bounce == 0 && lightHit) L = Le;
                     A.Lout[soff + (uint64_t)s * sstr] = make_float4(L.x, L.y, L.z, alpha);
                     ++s;
                 }
@@ -965,10 +899,11 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                 }
             }
         }
-        bool active = !waiting && s < A.spp;
+        bool active = !waiting && !need_shade && s < A.spp;
         RQ_MARK(1);
-        // new samples (pathintegrator.cpp:144-166; render.cpp:87-95); a zero bounce limit ends a
-        // sample at once, so loop until a ray is queued or the pixel is done
+        // 2. new samples (pathintegrator.cpp:144-166; render.cpp:87-95).  A camera ray that
+        //    k_primary found to escape, or a zero bounce limit, ends its sample here, so loop until
+        //    a hit is to be shaded, a ray is queued or the pixel is done.
         while (active) {
             const float2 sm = A.samples[soff + (uint64_t)s * sstr];
             const Ray ray = cast_ray(S, F2(sm.x, sm.y), A.W, A.H, px, py);
@@ -989,14 +924,146 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                 active = s < A.spp;
                 continue;
             }
-            queue_ext(ray.o, ray.d);
-            waiting = true;
+            if (A.prim) {
+                // camera ray traced by k_primary: shade its hit in this phase
+                const float t = light_loop(ray.o, ray.d);
+                const uint32_t g = A.prim[soff + (uint64_t)s * sstr];
+                if (g == NO_HIT) {
+                    if (lightHit) L = Le;
+                    A.Lout[soff + (uint64_t)s * sstr] = make_float4(L.x, L.y, L.z, alpha);
+                    ++s;
+                    active = s < A.spp;
+                    continue;
+                }
+                float4* e = my_out + lane * 2;
+                e[0] = make_float4(ray.o.x, ray.o.y, ray.o.z, t);
+                e[1] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.f);
+                need_shade = true;
+                hitg = g;
+            } else {
+                queue_ext(ray.o, ray.d);
+                waiting = true;
+            }
             active = false;
         }
         RQ_MARK(2);
-#ifdef NART_WAVEPROF
-        if (COUNT && lane == 0) cnt.pw[11] += __builtin_amdgcn_s_memtime() - prof_tp;  // path phase cycles
-#endif
+        // 3. shade the hits (pathintegrator.cpp:185-246)
+        if (need_shade) {
+            if (COUNT) ++n_bounce;
+            if (COUNT) WPROF(cnt, 8);
+            const float4 ro = my_out[lane * 2], rd = my_out[lane * 2 + 1];
+            const Ray cur = make_ray(F3(ro.x, ro.y, ro.z), F3(rd.x, rd.y, rd.z));
+            Isect is;
+            fill_isect(S, cur, hitg, is);
+            BSDF bsdf;
+            create_bsdf(S, is, alphaTweak, bsdf);
+            use1 = use2 = false;
+            bool cont;
+            f3 no, nd;
+            if (list.valid(is.meshID, is.priority, eta_outer)) {
+                if (bounce == 0) alpha = 1.f;
+                const f3 wo = to_local(bsdf, neg(cur.d));
+                // ---- EstimateDirect (pathintegrator.cpp:38-121)
+                const DLight& Lg = S.lights[f2u8(gmin(rng_float(rng), ND_ONE_MINUS_EPS) * nL)];
+                float sPdf = 0.f, lPdf = 0.f;
+                float sx = rng_float(rng);
+                float sy = rng_float(rng);
+                float bsmp = rng_float(rng);
+                uint32_t dflags = 0;
+                f3 wi;
+                f3 f = bsdf_sample_f(bsdf, wo, wi, bsmp, F2(sx, sy), sPdf, dflags, true, eta_outer, nullptr,
+                                     nullptr);
+                if (sPdf > 0.f) {
+                    float flip = wi.z > 0.f ? 1.f : -1.f;
+                    f3 wW = to_world(bsdf, wi);
+                    float lt = __builtin_inff();
+                    f3 Li = light_li<ENV>(S, Lg, is.p, wW, &lPdf, lt);
+                    float weight = 1.f;
+                    bool add1 = true;
+                    if (!(dflags & F_SPECULAR)) {
+                        weight = (sPdf * sPdf) / (sPdf * sPdf + lPdf * lPdf);
+                        add1 = lPdf > 0.f;
+                    }
+                    if (add1) {
+                        c1 = divs(muls(muls(mul(f, Li), gabs(wi.z)), weight), sPdf);
+                        // an all-zero term cannot change the sum: skip its shadow ray
+                        use1 = !(c1.x == 0.f && c1.y == 0.f && c1.z == 0.f);
+                        if (use1) put_ray(1, add(is.p, muls(muls(is.gn, SHADOW_BIAS), flip)), wW, lt);
+                    }
+                }
+                lPdf = 0.f;
+                float lx = rng_float(rng);
+                float ly = rng_float(rng);
+                f3 wiW;
+                float lt2 = __builtin_inff();
+                f3 Li2 = light_sample_li<ENV>(S, Lg, is.p, wiW, F2(lx, ly), lPdf, lt2);
+                f3 wi2 = to_local(bsdf, wiW);
+                if (lPdf > 0.f) {
+                    float sp2 = bsdf_pdf(bsdf, wo, wi2, true, eta_outer);
+                    if (sp2 > 0.f) {
+                        f3 fv = bsdf_f(bsdf, wo, wi2, true, eta_outer);
+                        float weight = (lPdf * lPdf) / (sp2 * sp2 + lPdf * lPdf);
+                        c2 = divs(muls(muls(mul(fv, Li2), gabs(wi2.z)), weight), lPdf);
+                        use2 = !(c2.x == 0.f && c2.y == 0.f && c2.z == 0.f);
+                        if (use2) {
+                            float flip2 = wi2.z > 0.f ? 1.f : -1.f;
+                            put_ray(2, add(is.p, muls(muls(is.gn, SHADOW_BIAS), flip2)), wiW, lt2);
+                        }
+                    }
+                }
+                betak = beta;
+                have_ed = true;
+                // ---- continuation (pathintegrator.cpp:199-220)
+                float a = rng_float(rng);
+                float b = rng_float(rng);
+                float bs2 = rng_float(rng);
+                float cpdf = 0.f, alpha_i = 0.f;
+                f3 wic;
+                f3 fc = bsdf_sample_f(bsdf, wo, wic, bs2, F2(a, b), cpdf, flags, false, eta_outer, &alpha_i,
+                                      &eta_sampled);
+                if (cpdf <= 0.f) {
+                    cont = false;
+                } else {
+                    alphaTweak = (1.f - (A.gamma * alpha_i)) * alphaTweak;
+                    beta = mul(beta, muls(divs(fc, cpdf), gabs(wic.z)));
+                    float flip = wic.z > 0.f ? 1.f : -1.f;
+                    no = add(is.p, muls(muls(is.gn, SHADOW_BIAS), flip));
+                    nd = to_world(bsdf, wic);
+                    cont = true;
+                }
+            } else {
+                // lower-priority interface: step through (pathintegrator.cpp:223-229)
+                no = add(is.p, muls(cur.d, SHADOW_BIAS));
+                nd = cur.d;
+                flags = F_TRANSMISSIVE;
+                float bs2 = rng_float(rng);
+                eta_sampled = bsdf_sample_eta(bsdf, bs2);
+                cont = true;
+                have_ed = false;
+            }
+            if (cont) {
+                if (flags & F_TRANSMISSIVE) list.update(is.meshID, is.priority, eta_sampled);
+                // Russian roulette (pathintegrator.cpp:236-246)
+                float q = gmax((beta.x + beta.y + beta.z) * 0.33333f, 0.f);
+                if (bounce > 3) {
+                    if (q >= rng_float(rng)) beta = divs(beta, q);
+                    else cont = false;
+                }
+            }
+            ++bounce;
+            if (COUNT) n_sh += (use1 ? 1u : 0u) + (use2 ? 1u : 0u);
+            ext_pending = false;
+            if (cont && bounce < A.bounces) queue_ext(no, nd);
+            if (newk) {
+                waiting = true;
+            } else {
+                // no query left (path ended, or ended at the bounce limit): the EstimateDirect
+                // term of this bounce, if any, is still owed
+                if (have_ed) L = add(L, mul(muls(F3(0.f, 0.f, 0.f), nL), betak));
+                A.Lout[soff + (uint64_t)s * sstr] = make_float4(L.x, L.y, L.z, alpha);
+                ++s;
+            }
+        }
         // queued rays: init the result words, then list the (lane, kind) ids in kind order
         if (newk) {
             uint4 r0 = *my_res;
@@ -1018,7 +1085,9 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
             nq += (uint32_t)__popcll(m);
         }
         RQ_MARK(3);
-        const bool more = A.qhead && !waiting && s >= A.spp && slot != 0xFFFFFFFEu;  // may still get a pixel
+        // a lane whose sample ended while shading starts its next sample in the next phase; one
+        // whose pixel is done may still get a pixel from the queue
+        const bool more = !waiting && (s < A.spp || (A.qhead && slot != 0xFFFFFFFEu));
         if (__ballot(waiting || tracing || more) == 0) break;  // every path of the wave is done
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
@@ -1453,6 +1522,112 @@ __global__ __launch_bounds__(256) void k_splat_col4(SplatArgs A) {
         float* o = A.tiles + ((uint64_t)bi * tpx + (ty0 + j) * A.tile + tx) * 5;
 #pragma unroll
         for (int k = 0; k < 5; ++k) o[k] = c[j][k];
+    }
+}
+
+// Splat with one bucket per block and the bucket's samples staged through LDS once.
+// A tile pixel receives its samples in (source pixel raster, sample) order, so the bucket is
+// swept source row by source row (and, when a whole row does not fit, in ascending column
+// chunks): each chunk's samples and radiance are read from HBM once into LDS ([sample][column]),
+// then every tile pixel whose candidate rows include this row adds the chunk's candidate columns
+// in ascending order.  The per-pair arithmetic is k_splat's (MODE as there), so tiles are
+// bit-identical.  (k_splat_col4 instead re-reads each bucket's ~1.5 MB through an L2 that the
+// many buckets in flight per XCD keep missing: 80 GB of fetches for 12.8 GB of data at C3.)
+// NT tile pixels per lane (tile^2 <= NT * blockDim); cw: columns per staged chunk.
+template <int MODE, int NT>
+__global__ __launch_bounds__(256) void k_splat_lds(SplatArgs A, uint32_t cw) {
+    extern __shared__ __attribute__((aligned(16))) float4 s_chunk[];  // L [spp][w], then uv [spp][w]
+    __shared__ float s_table[64];
+    __shared__ float s_thr[65];
+    if (threadIdx.x < 64) s_table[threadIdx.x] = A.table[threadIdx.x];
+    if (MODE > 0 && threadIdx.x < 65) s_thr[threadIdx.x] = A.thr[threadIdx.x];
+    const uint32_t bi = blockIdx.x;
+    const uint32_t bid = A.bucket_ids[bi];
+    const uint32_t bx = bid % A.nbx, by = bid / A.nbx;
+    const uint32_t x0 = A.B * bx, y0 = A.B * by;
+    const uint32_t x1 = min(A.B * (bx + 1), A.totalW), y1 = min(A.B * (by + 1), A.totalH);
+    const int bw = (int)(x1 - x0), bh = (int)(y1 - y0);
+    const uint32_t npx = (uint32_t)(bw * bh);
+    const uint32_t base = A.bucket_base[bi];
+    const int r = (int)ceilf(A.fw), fb = (int)A.fb;
+    const uint32_t tpx = A.tile * A.tile;
+    const uint32_t spp = A.spp;
+    float c[NT][5];
+#pragma unroll
+    for (int k = 0; k < NT; ++k)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) c[k][j] = 0.f;
+    for (int sy = 0; sy < bh; ++sy) {
+        const float fy = (float)(y0 + (uint32_t)sy + A.fb);
+        for (int c0 = 0; c0 < bw; c0 += (int)cw) {
+            const int w = min((int)cw, bw - c0);
+            float4* sL = s_chunk;
+            float2* sU = reinterpret_cast<float2*>(s_chunk + (size_t)spp * w);
+            __syncthreads();
+            {
+                const uint64_t row0 = (uint64_t)base * spp + (uint32_t)(sy * bw + c0);
+                for (uint32_t i = threadIdx.x; i < spp * (uint32_t)w; i += blockDim.x) {
+                    const uint32_t s = i / (uint32_t)w, col = i - s * (uint32_t)w;
+                    const uint64_t idx = row0 + (uint64_t)s * npx + col;
+                    sL[i] = A.Lout[idx];
+                    sU[i] = A.samples[idx];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < NT; ++k) {
+                const uint32_t t = threadIdx.x + (uint32_t)k * blockDim.x;
+                if (t >= tpx) continue;
+                const int tx = (int)(t % A.tile), ty = (int)(t / A.tile);
+                const int sylo = max(0, ty - fb - r), syhi = min(bh - 1, ty - fb + r);
+                const bool wrapy = bh == (int)A.B && ty <= fb + r + 1 && bh - 1 > syhi;
+                if (!((sy >= sylo && sy <= syhi) || (wrapy && sy == bh - 1))) continue;
+                const int sxlo = max(0, tx - fb - r), sxhi = min(bw - 1, tx - fb + r);
+                const bool wrapx = bw == (int)A.B && tx <= fb + r + 1 && bw - 1 > sxhi;
+                SplatLane P;
+                P.xsA = (float)((uint32_t)tx + x0);
+                P.xsB = (float)((uint32_t)tx + x0 + A.B);
+                P.ysA = (float)((uint32_t)ty + y0);
+                P.ysB = (float)((uint32_t)ty + y0 + A.B);
+                P.edgeX = (float)(x0 + A.B + A.fb);
+                P.edgeY = (float)(y0 + A.B + A.fb);
+                const uint32_t utx = (uint32_t)tx, uty = (uint32_t)ty;
+                (void)utx;
+                (void)uty;
+                // candidate columns of this chunk in ascending order, then the bucket-edge wrap column
+                const int lo = max(sxlo, c0), hi = min(sxhi, c0 + w - 1);
+                const int ncol = (hi >= lo ? hi - lo + 1 : 0) + ((wrapx && bw - 1 >= c0 && bw - 1 < c0 + w) ? 1 : 0);
+                for (int ci = 0; ci < ncol; ++ci) {
+                    const int sx = (lo + ci <= hi) ? lo + ci : bw - 1;
+                    const float fx = (float)(x0 + (uint32_t)sx + A.fb);
+                    const float4* lp = sL + (sx - c0);
+                    const float2* up = sU + (sx - c0);
+                    for (uint32_t s = 0; s < spp; ++s) {
+                        const float2 uv = up[(size_t)s * w];
+                        float wt;
+                        const bool h = MODE == 2 ? splat_hits_fast(A, P, s_table, s_thr, fx + uv.x, fy + uv.y, wt)
+                                     : MODE == 1 ? splat_hits_thr(A, s_table, s_thr, fx + uv.x, fy + uv.y, utx, uty, wt)
+                                                 : splat_hits(A, s_table, fx + uv.x, fy + uv.y, utx, uty, wt);
+                        if (h) {
+                            const float4 Lv = lp[(size_t)s * w];
+                            c[k][0] += Lv.x * wt;
+                            c[k][1] += Lv.y * wt;
+                            c[k][2] += Lv.z * wt;
+                            c[k][3] += Lv.w * wt;
+                            c[k][4] += wt;
+                        }
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+        const uint32_t t = threadIdx.x + (uint32_t)k * blockDim.x;
+        if (t >= tpx) continue;
+        float* o = A.tiles + ((uint64_t)bi * tpx + t) * 5;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) o[j] = c[k][j];
     }
 }
 

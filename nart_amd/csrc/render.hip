@@ -27,6 +27,8 @@ struct nart_ctx {
     uint32_t stack_depth = 1;
     uint32_t num_nodes = 0;
     int variant = 0;
+    // 3 four pixels per lane (default), 4 LDS-staged (C3: 117 vs 33 ms), 2/1/0 one pixel per lane
+    int splat_mode = 3;
     bool counters = false;
     bool has_env = false;  // scene has an environment light (selects the k_render build)
     // scene buffers
@@ -56,12 +58,14 @@ struct nart_ctx {
     uint32_t* d_rng = nullptr;
     float2* d_samples = nullptr;
     float4* d_L = nullptr;
+    uint32_t* d_prim = nullptr;  // camera-ray hits per sample (k_primary), same indexing as d_samples
     uint32_t* d_bucket_ids = nullptr;
     uint32_t* d_bucket_base = nullptr;
     float* d_table = nullptr;
     unsigned long long* d_counters = nullptr;
     size_t cap_slots = 0, cap_samples = 0, cap_buckets = 0;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // ev[4]: after k_primary
+    bool primary_ran = false;  // the last dispatch launched k_primary (ev[4] recorded)
     bool events = false;
     // wavefront variant: path state + queues (one allocation), pinned queue-count readback
     void* d_wf = nullptr;
@@ -273,7 +277,7 @@ int check_params(nart_ctx* ctx, const nart_render_params* p) {
 size_t batch_slot_limit(uint32_t spp) {
     size_t budget = (size_t)16 << 30;
     if (const char* e = std::getenv("NART_BATCH_BYTES")) budget = (size_t)std::strtoull(e, nullptr, 10);
-    size_t per = 8 + (size_t)spp * (sizeof(float2) + sizeof(float4));
+    size_t per = 8 + (size_t)spp * (sizeof(float2) + sizeof(float4) + sizeof(uint32_t));
     size_t n = budget / per;
     return n < 256 ? 256 : n;
 }
@@ -309,12 +313,13 @@ int ensure(nart_ctx* ctx, size_t slots, uint32_t spp, size_t buckets) {
     }
     if (samples > ctx->cap_samples) {
         ctx->cap_samples = 0;
-        for (void** b : {(void**)&ctx->d_samples, (void**)&ctx->d_L}) {
+        for (void** b : {(void**)&ctx->d_samples, (void**)&ctx->d_L, (void**)&ctx->d_prim}) {
             if (*b) hipFree(*b);
             *b = nullptr;
         }
         if ((rc = dmalloc(ctx, (void**)&ctx->d_samples, samples * sizeof(float2), "LatinSquare samples")) ||
-            (rc = dmalloc(ctx, (void**)&ctx->d_L, samples * sizeof(float4), "per-sample radiance")))
+            (rc = dmalloc(ctx, (void**)&ctx->d_L, samples * sizeof(float4), "per-sample radiance")) ||
+            (rc = dmalloc(ctx, (void**)&ctx->d_prim, samples * sizeof(uint32_t), "camera-ray hits")))
             return rc;
         ctx->cap_samples = samples;
     }
@@ -476,13 +481,16 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     static bool attr = false;  // dynamic LDS above the 64 KiB default
     if (!attr) {
         for (const void* f : {(const void*)kern, (const void*)kern_q, (const void*)k_render<MAXL, true, ENV, false>,
-                              (const void*)kern_rq})
+                              (const void*)kern_rq, (const void*)k_primary<COUNT, ENV>})
             hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
     // variant 0: ray-queue kernel; 2: k_render with the traversal quorum on every launch;
     // 3: k_render with the quorum chosen by rounds of resident waves (the previous default)
     const bool rq = ctx->variant == 0;
+    // camera rays first, coherently (k_primary); NART_PRIMARY=0 leaves them to the path kernel
+    static const bool primary = !std::getenv("NART_PRIMARY") || std::atoi(std::getenv("NART_PRIMARY")) != 0;
+
     // NART_QUORUM_MIN_ROUNDS: rounds of resident waves from which the quorum kernel is used (C3:
     // whole frame 16 rounds 569 -> 517 ms with it, 1/2 frame 8 rounds 332 -> 301, 1/4 4 rounds
     // 183 -> 179, 1/8 2 rounds 108 -> 134)
@@ -492,6 +500,16 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     b.lds_nodes = render_lds_nodes(ctx);
     const size_t lds = (size_t)ctx->stack_depth * 256 * 8 + (size_t)b.lds_nodes * sizeof(BVHNode);
     RenderArgs brq = a;  // ray-queue kernel: outbox, results and id lists take part of the LDS
+    if (rq && primary && ctx->d_prim && a.cost == nullptr) {
+        hipLaunchKernelGGL((k_primary<COUNT, ENV>), dim3((a.n_slots + 255) / 256), dim3(256),
+                           (size_t)ctx->stack_depth * 256 * 8, st, ctx->scene, a, ctx->d_prim);
+        HIPCHK(hipGetLastError());
+        if (ctx->events) {
+            HIPCHK(hipEventRecord(ctx->ev[4], st));
+            ctx->primary_ran = true;
+        }
+        brq.prim = ctx->d_prim;
+    }
     brq.lds_nodes = render_lds_nodes(ctx, rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK), NART_RQ_BLOCK / 256);
     const size_t lds_rq = rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK) + (size_t)brq.lds_nodes * sizeof(BVHNode);
     const dim3 block(256);
@@ -510,6 +528,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             static const uint32_t rqq = std::getenv("NART_RQ_QUORUM") ? (uint32_t)std::atoi(std::getenv("NART_RQ_QUORUM")) : 8u;
             RenderArgs r2 = args;
             r2.lds_nodes = brq.lds_nodes;
+            r2.prim = brq.prim;
             r2.rq_quorum = rqq;
             const uint32_t per = NART_RQ_BLOCK / 256;  // launches are counted in blocks of 256
             hipLaunchKernelGGL(kern_rq, dim3((nblocks + per - 1) / per), dim3(NART_RQ_BLOCK), lds_rq, st, ctx->scene, r2);
@@ -834,7 +853,7 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
     }
     const size_t limit = batch_slot_limit(p->spp);
     const uint32_t tpx = g.tile_size * g.tile_size;
-    double kernel_ms = 0.0, splat_ms = 0.0, latin_ms = 0.0;
+    double kernel_ms = 0.0, splat_ms = 0.0, latin_ms = 0.0, primary_ms = 0.0;
     uint32_t launches = 0;
     uint64_t traced = 0, counted = 0;
     uint32_t b0 = 0;
@@ -889,6 +908,7 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         rc = launch_latin(ctx, ra, st);
         if (rc) return rc;
         HIPCHK(hipEventRecord(ctx->ev[0], st));
+        ctx->primary_ran = false;
         rc = dispatch_render(ctx, ra, p->integrator, st);
         if (rc) return rc;
         HIPCHK(hipEventRecord(ctx->ev[1], st));
@@ -919,13 +939,32 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         uint64_t nthreads = (uint64_t)nbk * tpx;
         static const size_t splat_lds =
             std::getenv("NART_SPLAT_LDS") ? std::strtoull(std::getenv("NART_SPLAT_LDS"), nullptr, 10) : 0;
-        static const int splat_mode = std::getenv("NART_SPLAT_MODE") ? std::atoi(std::getenv("NART_SPLAT_MODE")) : 3;
+        const int splat_mode = ctx->splat_mode;
         const dim3 sg((uint32_t)((nthreads + 255) / 256));
 #ifndef NART_SPLAT_NP
 #define NART_SPLAT_NP 4
 #endif
         const uint64_t n4 = (uint64_t)nbk * g.tile_size * ((g.tile_size + NART_SPLAT_NP - 1) / NART_SPLAT_NP);
-        if (sa.thr && sa.invB != 0.f && splat_mode >= 3)
+        // mode 4 (default): bucket per block, samples staged through LDS in source-row chunks of cw
+        // columns (NART_SPLAT_CHUNK_KB of LDS per block)
+        static const size_t chunk_kb =
+            std::getenv("NART_SPLAT_CHUNK_KB") ? std::strtoull(std::getenv("NART_SPLAT_CHUNK_KB"), nullptr, 10) : 48;
+        const size_t col_bytes = (size_t)p->spp * (sizeof(float4) + sizeof(float2));
+        const uint32_t cw = (uint32_t)std::min<size_t>(p->bucket_size, std::max<size_t>(1, chunk_kb * 1024 / col_bytes));
+        const uint32_t nt = (tpx + 255) / 256;
+        const int lmode = sa.thr ? (sa.invB != 0.f ? 2 : 1) : 0;
+        if (splat_mode >= 4 && nt <= 4 && (size_t)cw * col_bytes <= (size_t)159 * 1024) {
+            const size_t lds = (size_t)cw * col_bytes;
+            auto launch_lds = [&](auto kern) {
+                hipLaunchKernelGGL(kern, dim3(nbk), dim3(256), lds, st, sa, cw);
+            };
+#define NART_SPLAT_LDS_CASE(M, N) \
+    if (lmode == M && nt == N) launch_lds(k_splat_lds<M, N>);
+            NART_SPLAT_LDS_CASE(0, 1) NART_SPLAT_LDS_CASE(0, 2) NART_SPLAT_LDS_CASE(0, 3) NART_SPLAT_LDS_CASE(0, 4)
+            NART_SPLAT_LDS_CASE(1, 1) NART_SPLAT_LDS_CASE(1, 2) NART_SPLAT_LDS_CASE(1, 3) NART_SPLAT_LDS_CASE(1, 4)
+            NART_SPLAT_LDS_CASE(2, 1) NART_SPLAT_LDS_CASE(2, 2) NART_SPLAT_LDS_CASE(2, 3) NART_SPLAT_LDS_CASE(2, 4)
+#undef NART_SPLAT_LDS_CASE
+        } else if (sa.thr && sa.invB != 0.f && splat_mode >= 3)
             hipLaunchKernelGGL(k_splat_col4<NART_SPLAT_NP>, dim3((uint32_t)((n4 + 255) / 256)), dim3(256), 0, st, sa);
         else if (sa.thr && sa.invB != 0.f && splat_mode >= 2) hipLaunchKernelGGL(k_splat<2>, sg, dim3(256), splat_lds, st, sa);
         else if (sa.thr && splat_mode >= 1) hipLaunchKernelGGL(k_splat<1>, sg, dim3(256), splat_lds, st, sa);
@@ -936,6 +975,10 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         float ms = 0.f;
         HIPCHK(hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]));
         kernel_ms += ms;
+        if (ctx->primary_ran) {
+            HIPCHK(hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[4]));
+            primary_ms += ms;
+        }
         HIPCHK(hipEventElapsedTime(&ms, ctx->ev[1], ctx->ev[2]));
         splat_ms += ms;
         HIPCHK(hipEventElapsedTime(&ms, ctx->ev[3], ctx->ev[0]));
@@ -947,6 +990,7 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         stats->kernel_ms += kernel_ms;
         stats->splat_ms += splat_ms;
         stats->latin_ms += latin_ms;
+        stats->primary_ms += primary_ms;
         stats->kernel_launches += launches;
         stats->traced_samples += traced;
         stats->samples += counted * p->spp;
@@ -1022,6 +1066,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     *out = nullptr;
     ctx->device = device_id;
     if (const char* v = std::getenv("NART_VARIANT")) ctx->variant = std::max(0, std::min(3, std::atoi(v)));
+    if (const char* v = std::getenv("NART_SPLAT_MODE")) ctx->splat_mode = std::max(0, std::min(4, std::atoi(v)));
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device_id || device_id < 0) {
         delete ctx;
@@ -1043,6 +1088,11 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     hipFuncSetAttribute((const void*)k_splat<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
     hipFuncSetAttribute((const void*)k_splat<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
     hipFuncSetAttribute((const void*)k_splat<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
+    for (const void* f : {(const void*)k_splat_lds<0, 1>, (const void*)k_splat_lds<0, 2>, (const void*)k_splat_lds<0, 3>,
+                          (const void*)k_splat_lds<0, 4>, (const void*)k_splat_lds<1, 1>, (const void*)k_splat_lds<1, 2>,
+                          (const void*)k_splat_lds<1, 3>, (const void*)k_splat_lds<1, 4>, (const void*)k_splat_lds<2, 1>,
+                          (const void*)k_splat_lds<2, 2>, (const void*)k_splat_lds<2, 3>, (const void*)k_splat_lds<2, 4>})
+        hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
     (void)hipGetLastError();  // the splat LDS limit is a tuning knob (NART_SPLAT_LDS), not required
     // reference octree visibility (Q14) + device BVH
     std::vector<uint8_t> mask;
@@ -1196,7 +1246,7 @@ void nart_hip_destroy(nart_ctx* ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
     void* bufs[] = {ctx->d_nodes, ctx->d_tri_isect, ctx->d_tri_perm, ctx->d_tris, ctx->d_tri_mesh, ctx->d_meshes, ctx->d_mats,
-                    ctx->d_lights, ctx->d_texs, ctx->d_tex_pool, ctx->d_slot_xy, ctx->d_slot_so, ctx->d_rng, ctx->d_samples,
+                    ctx->d_lights, ctx->d_texs, ctx->d_tex_pool, ctx->d_slot_xy, ctx->d_slot_so, ctx->d_rng, ctx->d_samples, ctx->d_prim,
                     ctx->d_L, ctx->d_bucket_ids, ctx->d_bucket_base, ctx->d_table, ctx->d_counters, ctx->d_wf, ctx->d_envs, ctx->d_density,
                     ctx->d_oc_nodes, ctx->d_oc_chunks, ctx->d_oc_tris, ctx->d_tri_leaf, ctx->d_oc_lock, ctx->d_oc_heap,
                     ctx->d_queue, ctx->d_cost, ctx->d_keys[0], ctx->d_keys[1], ctx->d_vals[0], ctx->d_vals[1],
@@ -1218,6 +1268,15 @@ const char* nart_hip_last_error(const nart_ctx* ctx) { return ctx ? ctx->err.c_s
 int nart_hip_set_counters(nart_ctx* ctx, int enable) {
     if (!ctx) return NART_E_INVALID;
     ctx->counters = enable != 0;
+    return NART_OK;
+}
+
+int nart_hip_set_splat_mode(nart_ctx* ctx, int mode) {
+    if (!ctx) return NART_E_INVALID;
+    if (mode < 0 || mode > 4)
+        return fail(ctx, NART_E_UNSUPPORTED, "splat mode must be 0-4 (4 LDS-staged, 3 four pixels per lane, 2-0 one "
+                                             "pixel per lane)");
+    ctx->splat_mode = mode;
     return NART_OK;
 }
 

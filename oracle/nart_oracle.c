@@ -277,6 +277,7 @@ struct oracle_scene {
     size_t* tex_off;
     /* environment distributions per light (Piecewise2DDistribution) */
     struct pw2d { int present; uint32_t w, h; float invW, invH; float *mpdf, *cpdf, *mcdf, *ccdf; } * env;
+    uint32_t nenv; /* entries of env: oracle_destroy must not read the caller's blob, which may be gone */
     /* camera medium (media.h:98-120): the majorant table is laid out as the reference's Medium
        members after MajorantGrid::majorants[1] -- {majorant * sigma_maj, sigma_maj, boundsMin,
        boundsMax} -- because RayMajorantIterator::Next can index past the 1-entry array. */
@@ -1665,6 +1666,7 @@ int oracle_render_samples(oracle_scene* s, const nart_render_params* p, uint32_t
 static void build_env(oracle_scene* s) { /* Piecewise2DDistribution ctor (texturepattern.cpp:3-70) */
     const nart_scene_blob* b = s->blob;
     s->env = (struct pw2d*)calloc(b->num_lights ? b->num_lights : 1, sizeof(struct pw2d));
+    s->nenv = s->env ? b->num_lights : 0;
     for (uint32_t l = 0; l < b->num_lights; ++l) {
         const nart_light* L = &b->lights[l];
         if (L->Le.type != NART_PTN_TEXTURE) continue;
@@ -1775,7 +1777,7 @@ void oracle_destroy(oracle_scene* s) {
     free(s->tex_f);
     free(s->tex_off);
     if (s->env) {
-        for (uint32_t l = 0; l < s->blob->num_lights; ++l) {
+        for (uint32_t l = 0; l < s->nenv; ++l) {
             free(s->env[l].mpdf);
             free(s->env[l].cpdf);
             free(s->env[l].mcdf);

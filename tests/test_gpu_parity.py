@@ -305,10 +305,12 @@ def test_latin_square_high_spp_frame(gpu, glass_scene, glass_oracle):
 
 
 @pytest.mark.parametrize("bucket,fw", [(12, 2.0), (16, 1.0), (8, 2.5), (10, 0.75), (16, 3.0), (4, 0.25)])
-def test_splat_bucket_and_filter_sizes(gpu, glass_scene, glass_oracle, bucket, fw):
+@pytest.mark.parametrize("splat_mode", [4, 3, 0], ids=["lds", "col4", "direct"])
+def test_splat_bucket_and_filter_sizes(gpu, glass_scene, glass_oracle, bucket, fw, splat_mode):
     """Splat arithmetic paths: power-of-two buckets use the compare-only pair test, other sizes
-    the direct one; filter widths with threshold-derived indices (fw > ~0.28) and without (0.25)."""
+    the direct one; filter widths with threshold-derived indices (fw > ~0.28) and without (0.25);
+    the LDS-staged, four-pixels-per-lane and one-pixel-per-lane kernels."""
     p = _params(glass_scene, 40, 30, 4, bucket_size=bucket, filter_width=fw, bounces=3)
-    g = nart_amd.HipRenderer(glass_scene).render(p)
+    g = nart_amd.HipRenderer(glass_scene, splat_mode=splat_mode).render(p)
     o = glass_oracle.render(p)
     assert _bits_equal(g, o), _report(g, o)

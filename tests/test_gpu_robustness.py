@@ -40,7 +40,8 @@ def test_failed_allocation_then_render(gpu, glass_scene):
 
 def test_batch_beyond_2_32_samples(gpu, glass_scene, monkeypatch):
     """One batch of 1920x1080 (+ the 4 extra traced rows) x 2070 spp = 4.31e9 samples > 2^32
-    (NART_BATCH_BYTES raised to 110 GB): 64-bit sample offsets.  The frame equals the same frame
+    (NART_BATCH_BYTES raised to 130 GB; 28 B per sample: LatinSquare sample, radiance, camera-ray
+    hit): 64-bit sample offsets.  The frame equals the same frame
     rendered in 16-GiB batches (each < 2^32 samples), and the last buckets -- whose samples sit
     beyond 2^32 in the single batch -- equal the oracle's."""
     import torch
@@ -60,7 +61,7 @@ def test_batch_beyond_2_32_samples(gpu, glass_scene, monkeypatch):
         torch.cuda.synchronize()
         return tiles.cpu().numpy(), st
 
-    one, st1 = frame(110_000_000_000)
+    one, st1 = frame(130_000_000_000)
     assert st1.kernel_launches == 1 and st1.traced_samples > 2 ** 32, (st1.kernel_launches, st1.traced_samples)
     many, st2 = frame(16 << 30)
     assert st2.kernel_launches > 1
