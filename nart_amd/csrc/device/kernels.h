@@ -1602,20 +1602,41 @@ __global__ __launch_bounds__(256) void k_splat_lds(SplatArgs A, uint32_t cw) {
                     const float fx = (float)(x0 + (uint32_t)sx + A.fb);
                     const float4* lp = sL + (sx - c0);
                     const float2* up = sU + (sx - c0);
-                    for (uint32_t s = 0; s < spp; ++s) {
-                        const float2 uv = up[(size_t)s * w];
-                        float wt;
-                        const bool h = MODE == 2 ? splat_hits_fast(A, P, s_table, s_thr, fx + uv.x, fy + uv.y, wt)
-                                     : MODE == 1 ? splat_hits_thr(A, s_table, s_thr, fx + uv.x, fy + uv.y, utx, uty, wt)
-                                                 : splat_hits(A, s_table, fx + uv.x, fy + uv.y, utx, uty, wt);
+                    auto hit1 = [&](float2 uv, float& wt) {
+                        return MODE == 2 ? splat_hits_fast(A, P, s_table, s_thr, fx + uv.x, fy + uv.y, wt)
+                             : MODE == 1 ? splat_hits_thr(A, s_table, s_thr, fx + uv.x, fy + uv.y, utx, uty, wt)
+                                         : splat_hits(A, s_table, fx + uv.x, fy + uv.y, utx, uty, wt);
+                    };
+                    auto add1 = [&](bool h, float wt, float4 Lv) {
                         if (h) {
-                            const float4 Lv = lp[(size_t)s * w];
                             c[k][0] += Lv.x * wt;
                             c[k][1] += Lv.y * wt;
                             c[k][2] += Lv.z * wt;
                             c[k][3] += Lv.w * wt;
                             c[k][4] += wt;
                         }
+                    };
+                    // groups of 4 samples: loads and pair tests independent, sums in sample order
+                    uint32_t s = 0;
+                    for (; s + 4 <= spp; s += 4) {
+                        float2 uv[4];
+                        float4 Lv[4];
+                        float wt[4];
+                        bool h[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            uv[u] = up[(size_t)(s + u) * w];
+                            Lv[u] = lp[(size_t)(s + u) * w];
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) h[u] = hit1(uv[u], wt[u]);
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) add1(h[u], wt[u], Lv[u]);
+                    }
+                    for (; s < spp; ++s) {
+                        float wt;
+                        const bool h = hit1(up[(size_t)s * w], wt);
+                        add1(h, wt, lp[(size_t)s * w]);
                     }
                 }
             }

@@ -168,6 +168,8 @@ ND bool trav_pop(Trav& t, const int* sc, const float* st, int stride) {
 template <bool COUNT>
 ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, int stride, TraceCounters& cnt,
                   const float4* lnodes, int nl) {
+    // (a wave-uniform node loop -- ballot per iteration, stopping once at most 0/2/4/8 lanes still
+    // descend -- measured 13 % slower in k_render_rq than this per-lane loop: 114 vs 101 ms)
     while (t.code >= 0) {
         if (COUNT) cnt.nodes++;
         if (COUNT) WPROF(cnt, 2);

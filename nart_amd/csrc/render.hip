@@ -501,6 +501,8 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     const size_t lds = (size_t)ctx->stack_depth * 256 * 8 + (size_t)b.lds_nodes * sizeof(BVHNode);
     RenderArgs brq = a;  // ray-queue kernel: outbox, results and id lists take part of the LDS
     if (rq && primary && ctx->d_prim && a.cost == nullptr) {
+        // (staging the top BVH nodes in LDS, as the path kernel does, measured slower here: a
+        // wave's coherent rays read the same node, which the L1 broadcasts: 9.7 vs 8.2 ms at 64 spp)
         hipLaunchKernelGGL((k_primary<COUNT, ENV>), dim3((a.n_slots + 255) / 256), dim3(256),
                            (size_t)ctx->stack_depth * 256 * 8, st, ctx->scene, a, ctx->d_prim);
         HIPCHK(hipGetLastError());
@@ -525,11 +527,14 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     // the ray-queue kernel takes kern's place (its own LDS layout); the cost probe keeps k_render
     auto launch = [&](uint32_t nblocks, const RenderArgs& args) {
         if (rq) {
-            static const uint32_t rqq = std::getenv("NART_RQ_QUORUM") ? (uint32_t)std::atoi(std::getenv("NART_RQ_QUORUM")) : 8u;
+            // traversal-phase quorum: 8 on throughput-bound launches; 0 (every queued ray resolved
+            // before the path phase) on small shards, whose costliest pixels' chains set the time
+            // (1/8 C3 shard: 100.5 -> 96.0 ms)
+            static const int rqq = std::getenv("NART_RQ_QUORUM") ? std::atoi(std::getenv("NART_RQ_QUORUM")) : -1;
             RenderArgs r2 = args;
             r2.lds_nodes = brq.lds_nodes;
             r2.prim = brq.prim;
-            r2.rq_quorum = rqq;
+            r2.rq_quorum = rqq >= 0 ? (uint32_t)rqq : (R >= q_rounds ? 8u : 0u);
             const uint32_t per = NART_RQ_BLOCK / 256;  // launches are counted in blocks of 256
             hipLaunchKernelGGL(kern_rq, dim3((nblocks + per - 1) / per), dim3(NART_RQ_BLOCK), lds_rq, st, ctx->scene, r2);
         } else {
@@ -552,8 +557,12 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                 HIPCHK(hipGetLastError());
                 return NART_OK;
             }
-            if (const char* e = std::getenv("NART_QUEUE_K")) k = (uint32_t)std::max(1, std::min(64, std::atoi(e)));
-            const bool refill = k < 64u || mode == 1;
+            if (const char* e = std::getenv("NART_QUEUE_K")) k = (uint32_t)std::max(1, std::min(65, std::atoi(e)));
+            // k = 65: every first-round lane dealt round robin from the cost-sorted group list
+            // (each wave one pixel of each of 64 cost bands), the rest refilled costliest first
+            const bool deal_all = k == 65u;
+            if (deal_all) k = 64u;
+            const bool refill = k < 64u || mode == 1 || deal_all;
             if (mode == 1) {
                 hipLaunchKernelGGL(k_iota, eg, block, 0, st, ctx->d_queue, n);
             } else {
@@ -561,15 +570,19 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                 pb.spp = 1;
                 pb.cost = ctx->d_cost;
                 hipLaunchKernelGGL((k_render<MAXL, true, ENV, false>), dim3(blocks), block, lds, st, ctx->scene, pb);
-                int rc2 = sort_groups_by_cost(ctx, n, k == 64u ? ctx->d_queue : ctx->d_cost, st);
+                int rc2 = sort_groups_by_cost(ctx, n, (k == 64u && !deal_all) ? ctx->d_queue : ctx->d_cost, st);
                 if (rc2) return rc2;
                 size_t tmp = 0;
-                if (k == 64u) {  // whole groups, costliest first (coherent waves, longest chains first)
+                if (deal_all) {
+                    hipLaunchKernelGGL(k_build_queue, eg, block, 0, st, ctx->d_cost, ctx->d_cost + (size_t)64 * W, n, W,
+                                       64u, ctx->d_queue);
+                } else if (k == 64u) {  // whole groups, costliest first (coherent waves, longest chains first)
                     b.queue = ctx->d_queue;
                     launch(blocks, b);
                     HIPCHK(hipGetLastError());
                     return NART_OK;
                 }
+                if (!deal_all) {
                 HIPCHK(hipMemcpyAsync(ctx->d_vals[1], ctx->d_cost, (size_t)n * 4, hipMemcpyDeviceToDevice, st));
                 // d_vals[1] = pixels by cost class; partition the rest (slot order) from the top k*W
                 hipLaunchKernelGGL(k_flag_top, eg, block, 0, st, ctx->d_vals[1], n, k * W, ctx->d_keys[0]);
@@ -579,6 +592,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                                                           ctx->d_cost, ctx->d_vals[0], (int)n, 0, 1, st));
                 hipLaunchKernelGGL(k_build_queue, eg, block, 0, st, ctx->d_vals[1], ctx->d_vals[0], n, W, k,
                                    ctx->d_queue);
+                }
             }
             b.queue = ctx->d_queue;
             if (refill) {
@@ -951,12 +965,13 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
             std::getenv("NART_SPLAT_CHUNK_KB") ? std::strtoull(std::getenv("NART_SPLAT_CHUNK_KB"), nullptr, 10) : 48;
         const size_t col_bytes = (size_t)p->spp * (sizeof(float4) + sizeof(float2));
         const uint32_t cw = (uint32_t)std::min<size_t>(p->bucket_size, std::max<size_t>(1, chunk_kb * 1024 / col_bytes));
-        const uint32_t nt = (tpx + 255) / 256;
+        static const uint32_t lblk = std::getenv("NART_SPLAT_LDS_BLOCK") ? (uint32_t)std::atoi(std::getenv("NART_SPLAT_LDS_BLOCK")) : 256u;
+        const uint32_t nt = (tpx + lblk - 1) / lblk;
         const int lmode = sa.thr ? (sa.invB != 0.f ? 2 : 1) : 0;
         if (splat_mode >= 4 && nt <= 4 && (size_t)cw * col_bytes <= (size_t)159 * 1024) {
             const size_t lds = (size_t)cw * col_bytes;
             auto launch_lds = [&](auto kern) {
-                hipLaunchKernelGGL(kern, dim3(nbk), dim3(256), lds, st, sa, cw);
+                hipLaunchKernelGGL(kern, dim3(nbk), dim3(lblk), lds, st, sa, cw);
             };
 #define NART_SPLAT_LDS_CASE(M, N) \
     if (lmode == M && nt == N) launch_lds(k_splat_lds<M, N>);
