@@ -541,9 +541,9 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
                 f3 Li2 = light_sample_li<ENV>(S, Lg, is.p, wiW, F2(lx, ly), lPdf, lt2);
                 f3 wi2 = to_local(bsdf, wiW);
                 if (lPdf > 0.f) {
-                    float sp2 = bsdf_pdf(bsdf, wo, wi2, true, eta_outer);
+                    float sp2;
+                    const f3 fv = bsdf_f_pdf(bsdf, wo, wi2, true, eta_outer, sp2);
                     if (sp2 > 0.f) {
-                        f3 fv = bsdf_f(bsdf, wo, wi2, true, eta_outer);
                         float weight = (lPdf * lPdf) / (sp2 * sp2 + lPdf * lPdf);
                         c2 = divs(muls(muls(mul(fv, Li2), gabs(wi2.z)), weight), lPdf);
                         use2 = !(c2.x == 0.f && c2.y == 0.f && c2.z == 0.f);
@@ -999,9 +999,9 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                 f3 Li2 = light_sample_li<ENV>(S, Lg, is.p, wiW, F2(lx, ly), lPdf, lt2);
                 f3 wi2 = to_local(bsdf, wiW);
                 if (lPdf > 0.f) {
-                    float sp2 = bsdf_pdf(bsdf, wo, wi2, true, eta_outer);
+                    float sp2;
+                    const f3 fv = bsdf_f_pdf(bsdf, wo, wi2, true, eta_outer, sp2);
                     if (sp2 > 0.f) {
-                        f3 fv = bsdf_f(bsdf, wo, wi2, true, eta_outer);
                         float weight = (lPdf * lPdf) / (sp2 * sp2 + lPdf * lPdf);
                         c2 = divs(muls(muls(mul(fv, Li2), gabs(wi2.z)), weight), lPdf);
                         use2 = !(c2.x == 0.f && c2.y == 0.f && c2.z == 0.f);

@@ -517,6 +517,77 @@ ND float bxdf_pdf(const BxDF& b, f3 wo, f3 wi, bool uap, float eta_outer) {
 }
 ND float bxdf_eta(const BxDF& b) { return b.type == B_LAMBERT ? 0.f : b.eta; }
 
+// bxdf_f and bxdf_pdf of the same (wo, wi) in one pass: each value is computed with exactly the
+// operations of those two functions, but the half vector, D and the Smith term of wo, which both
+// recompute, are evaluated once (every call site of the reference pairs them: BxDF::Sample_f ends
+// with Pdf and f, EstimateDirect's light strategy with Pdf and f).
+ND f3 bxdf_f_pdf(const BxDF& b, f3 wo, f3 wi, bool uap, float eta_outer, float& pdf) {
+    pdf = 0.f;
+    if (b.type == B_LAMBERT) {  // lambertbrdf.cpp:7-29
+        pdf = wi.z * ND_ONE_OVER_PI;
+        return muls(b.rho, ND_ONE_OVER_PI);
+    }
+    if (b.type == B_DIEL) {  // dielectricbrdf.cpp:31-80 (f), 187-225 (Pdf)
+        const float alpha = uap ? b.ap : b.a0;
+        float eta_o = eta_outer, eta_i = b.eta;
+        const bool same = eta_o == eta_i;
+        const float lo = lambda_(alpha, wo);
+        if (wo.z * wi.z >= 0.f) {
+            // reflection: f swaps the etas for wo.z < 0, Pdf does not need them
+            if (wo.z < 0.f) { float t = eta_o; eta_o = eta_i; eta_i = t; }
+            f3 wh = normalize(add(wo, wi));
+            if (wh.z < 0.f) wh = muls(wh, -1.f);
+            const float d = D_diel(alpha, wh);
+            if (!same) {
+                const float cosThetaH = gabs(gmin(dot(wo, wh), 1.f));
+                const float p = (d * gmin(dot(wo, wh), 1.f) * (1.f / (1.f + lo))) / wo.z;
+                pdf = gmax(0.f, p / (4.f * cosThetaH));
+            }
+            const float g = 1.f / (1.f + lo + lambda_(alpha, wi));
+            const float Fr = fresnel(eta_o, eta_i, gabs(dot(wh, wo)));
+            if (wo.z * wi.z == 0.f) return F3(0.f, 0.f, 0.f);
+            return divs(muls(muls(muls(b.rho, g), d), Fr), (4.f * wo.z * wi.z));
+        }
+        if (wo.z < 0.f) { float t = eta_o; eta_o = eta_i; eta_i = t; }
+        f3 wh = normalize(add(muls(wo, eta_o), muls(wi, eta_i)));
+        if (wh.z < 0.f) wh = muls(wh, -1.f);
+        const float d = D_diel(alpha, wh);
+        const float wiDotWh = dot(wi, wh);
+        const float woDotWh = dot(wo, wh);
+        if (!same) {
+            const float p = (d * gmin(gabs(woDotWh), 1.f) * (1.f / (1.f + lo))) / gabs(wo.z);
+            const float denom = (eta_i * wiDotWh + eta_o * woDotWh);
+            const float JDet = (fabsf(wiDotWh) * eta_i * eta_i) / (denom * denom);
+            pdf = p * JDet;
+        }
+        const float Fr = fresnel(eta_o, eta_i, gabs(woDotWh));
+        if (Fr >= 1.f) return F3(0.f, 0.f, 0.f);
+        const float g = 1.f / (1.f + lo + lambda_(alpha, wi));
+        const float num = g * d * (1.f - Fr) * gabs(wiDotWh) * gabs(woDotWh) * eta_o * eta_o;
+        const float x = ((eta_i * wiDotWh) + (eta_o * woDotWh));
+        const float denom = x * x * gabs(wo.z * wi.z);
+        const float q = num / denom;
+        return mul(F3(q, q, q), b.tau);
+    }
+    if (b.type == B_TS) {  // torrancesparrowbrdf.cpp:32-51 (f), 109-124 (Pdf)
+        const float alpha = uap ? b.ap : b.a0;
+        const f3 wh = normalize(add(wo, wi));
+        const float d = D_ggx(alpha, wh);
+        const float lo = lambda_(alpha, wo);
+        if (!(wh.z < 0.f)) {
+            const float cosThetaH = gmin(dot(wo, wh), 1.f);
+            const float p = (d * gmin(dot(wo, wh), 1.f) * (1.f / (1.f + lo))) / wo.z;
+            pdf = gmax(0.f, p / (4.f * cosThetaH));
+        }
+        if (wo.z < 0.f || wi.z < 0.f) return F3(0.f, 0.f, 0.f);
+        const float g = 1.f / (1.f + lo + lambda_(alpha, wi));
+        const float fr = fresnel(eta_outer, b.eta, dot(wh, wi));
+        if (wo.z * wi.z == 0.f) return F3(0.f, 0.f, 0.f);
+        return divs(muls(muls(muls(b.rho, g), d), fr), (4.f * wo.z * wi.z));
+    }
+    return F3(0.f, 0.f, 0.f);  // delta lobes: f == 0, Pdf == 0
+}
+
 ND f3 bxdf_sample_f(const BxDF& b, f3 wo, f3& wi, float s1, f2 sample, float& pdf, uint32_t& flags, float* alpha_i,
                     bool uap, float eta_outer) {
     if (b.type == B_LAMBERT) {  // lambertbrdf.cpp:13-22
@@ -588,16 +659,20 @@ ND f3 bxdf_sample_f(const BxDF& b, f3 wo, f3& wi, float s1, f2 sample, float& pd
         float Fr = fresnel(eta_o, eta_i, gabs(dot(wh, wo)));
         if (s1 < Fr) {
             wi = normalize(reflect(wo, wh));
-            pdf = bxdf_pdf(b, wo, wi, uap, eta_outer) * Fr;
-            return bxdf_f(b, wo, wi, uap, eta_outer);
+            float pp;
+            const f3 fr = bxdf_f_pdf(b, wo, wi, uap, eta_outer, pp);
+            pdf = pp * Fr;
+            return fr;
         }
         float cos_o = gmin(1.f, gmax(-1.f, dot(wo, wh)));
         float sin_o = sqrtf(1.f - (cos_o * cos_o));
         float sin_i = ((eta_o / eta_i) * sin_o);
         if (sin_i >= 1.f) {
             wi = normalize(reflect(wo, wh));
-            pdf = bxdf_pdf(b, wo, wi, uap, eta_outer) * (1.f - Fr);
-            return bxdf_f(b, wo, wi, uap, eta_outer);
+            float pp;
+            const f3 fr = bxdf_f_pdf(b, wo, wi, uap, eta_outer, pp);
+            pdf = pp * (1.f - Fr);
+            return fr;
         }
         flags |= F_TRANSMISSIVE;
         f3 bb = muls(wh, cos_o);
@@ -606,8 +681,10 @@ ND f3 bxdf_sample_f(const BxDF& b, f3 wo, f3& wi, float s1, f2 sample, float& pd
         f3 d = muls(neg(wh), sqrtf(1.f - (sin_i * sin_i)));
         if (dot(wo, wh) < 0.f) d = muls(d, -1.f);
         wi = normalize(add(c, d));
-        pdf = bxdf_pdf(b, wo, wi, uap, eta_outer) * (1.f - Fr);
-        return bxdf_f(b, wo, wi, uap, eta_outer);
+        float pp;
+        const f3 fr = bxdf_f_pdf(b, wo, wi, uap, eta_outer, pp);
+        pdf = pp * (1.f - Fr);
+        return fr;
     }
     // B_TS: torrancesparrowbrdf.cpp:53-105
     float alpha = uap ? b.ap : b.a0;
@@ -617,8 +694,7 @@ ND f3 bxdf_sample_f(const BxDF& b, f3 wo, f3& wi, float s1, f2 sample, float& pd
     if (alpha >= 1.0f) flags = F_DIFFUSE;
     f3 wh = sample_wh(wo, alpha, sample, false);
     wi = normalize(reflect(wo, wh));
-    pdf = bxdf_pdf(b, wo, wi, uap, eta_outer);
-    return bxdf_f(b, wo, wi, uap, eta_outer);
+    return bxdf_f_pdf(b, wo, wi, uap, eta_outer, pdf);
 }
 
 // ---------------------------------------------------------------- BSDF (bxdf.cpp:24-115)
@@ -650,6 +726,20 @@ ND float bsdf_pdf(const BSDF& s, f3 wo, f3 wi, bool uap, float eta_outer) {
     if (s.num > 1) pdf += bxdf_pdf(s.b[1], wo, wi, uap, eta_outer);
     return pdf / (float)s.num;
 }
+// bsdf_f and bsdf_pdf together (bxdf_f_pdf per lobe; the sums in the same order)
+ND f3 bsdf_f_pdf(const BSDF& s, f3 wo, f3 wi, bool uap, float eta_outer, float& pdf) {
+    float p0, p1 = 0.f;
+    f3 f = F3(0.f, 0.f, 0.f);
+    f = add(f, bxdf_f_pdf(s.b[0], wo, wi, uap, eta_outer, p0));
+    f3 f1 = F3(0.f, 0.f, 0.f);
+    if (s.num > 1) f1 = bxdf_f_pdf(s.b[1], wo, wi, uap, eta_outer, p1);
+    if (s.num > 1) f = add(f, f1);
+    float p = 0.f;
+    p += p0;
+    if (s.num > 1) p += p1;
+    pdf = p / (float)s.num;
+    return f;
+}
 ND f3 bsdf_sample_f(const BSDF& s, f3 wo, f3& wi, float s1, f2 sample, float& pdf, uint32_t& flags, bool uap,
                     float eta_outer, float* alpha_i, float* eta_i) {
     uint32_t idx = f2u8(s1 * (float)s.num);
@@ -661,10 +751,11 @@ ND f3 bsdf_sample_f(const BSDF& s, f3 wo, f3& wi, float s1, f2 sample, float& pd
         if (s.num > 1) {
             const BxDF& o = s.b[idx ? 0 : 1];
             if (!(o.flags & F_SPECULAR)) {
-                float bp = bxdf_pdf(o, wo, wi, uap, eta_outer);
+                float bp;
+                const f3 fo = bxdf_f_pdf(o, wo, wi, uap, eta_outer, bp);
                 if (bp > 0.f) {
-                    pdf += bxdf_pdf(o, wo, wi, uap, eta_outer);
-                    f = add(f, bxdf_f(o, wo, wi, uap, eta_outer));
+                    pdf += bp;
+                    f = add(f, fo);
                 }
             }
         }

@@ -356,9 +356,9 @@ ND uint32_t shade_slot(const DScene& S, const WFArgs& A, uint32_t slot, const ui
             const f3 Li2 = light_sample_li(S, Lg, is.p, wiW, F2(lx, ly), lPdf, lt2);
             const f3 wi2 = to_local(bsdf, wiW);
             if (lPdf > 0.f) {
-                const float sp2 = bsdf_pdf(bsdf, wo, wi2, true, eta_outer);
+                float sp2;
+                const f3 fv = bsdf_f_pdf(bsdf, wo, wi2, true, eta_outer, sp2);
                 if (sp2 > 0.f) {
-                    const f3 fv = bsdf_f(bsdf, wo, wi2, true, eta_outer);
                     const float weight = (lPdf * lPdf) / (sp2 * sp2 + lPdf * lPdf);
                     const f3 c2 = divs(muls(muls(mul(fv, Li2), gabs(wi2.z)), weight), lPdf);
                     use2 = !(c2.x == 0.f && c2.y == 0.f && c2.z == 0.f);
