@@ -557,12 +557,8 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                 HIPCHK(hipGetLastError());
                 return NART_OK;
             }
-            if (const char* e = std::getenv("NART_QUEUE_K")) k = (uint32_t)std::max(1, std::min(65, std::atoi(e)));
-            // k = 65: every first-round lane dealt round robin from the cost-sorted group list
-            // (each wave one pixel of each of 64 cost bands), the rest refilled costliest first
-            const bool deal_all = k == 65u;
-            if (deal_all) k = 64u;
-            const bool refill = k < 64u || mode == 1 || deal_all;
+            if (const char* e = std::getenv("NART_QUEUE_K")) k = (uint32_t)std::max(1, std::min(64, std::atoi(e)));
+            const bool refill = k < 64u || mode == 1;
             if (mode == 1) {
                 hipLaunchKernelGGL(k_iota, eg, block, 0, st, ctx->d_queue, n);
             } else {
@@ -570,19 +566,15 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                 pb.spp = 1;
                 pb.cost = ctx->d_cost;
                 hipLaunchKernelGGL((k_render<MAXL, true, ENV, false>), dim3(blocks), block, lds, st, ctx->scene, pb);
-                int rc2 = sort_groups_by_cost(ctx, n, (k == 64u && !deal_all) ? ctx->d_queue : ctx->d_cost, st);
+                int rc2 = sort_groups_by_cost(ctx, n, k == 64u ? ctx->d_queue : ctx->d_cost, st);
                 if (rc2) return rc2;
                 size_t tmp = 0;
-                if (deal_all) {
-                    hipLaunchKernelGGL(k_build_queue, eg, block, 0, st, ctx->d_cost, ctx->d_cost + (size_t)64 * W, n, W,
-                                       64u, ctx->d_queue);
-                } else if (k == 64u) {  // whole groups, costliest first (coherent waves, longest chains first)
+                if (k == 64u) {  // whole groups, costliest first (coherent waves, longest chains first)
                     b.queue = ctx->d_queue;
                     launch(blocks, b);
                     HIPCHK(hipGetLastError());
                     return NART_OK;
                 }
-                if (!deal_all) {
                 HIPCHK(hipMemcpyAsync(ctx->d_vals[1], ctx->d_cost, (size_t)n * 4, hipMemcpyDeviceToDevice, st));
                 // d_vals[1] = pixels by cost class; partition the rest (slot order) from the top k*W
                 hipLaunchKernelGGL(k_flag_top, eg, block, 0, st, ctx->d_vals[1], n, k * W, ctx->d_keys[0]);
@@ -592,7 +584,6 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                                                           ctx->d_cost, ctx->d_vals[0], (int)n, 0, 1, st));
                 hipLaunchKernelGGL(k_build_queue, eg, block, 0, st, ctx->d_vals[1], ctx->d_vals[0], n, W, k,
                                    ctx->d_queue);
-                }
             }
             b.queue = ctx->d_queue;
             if (refill) {
@@ -824,6 +815,7 @@ bool splat_thresholds(float fw, float thr[65]) {
 // spp (scratch in Lout: 2*spp floats per lane of every launched block, within Lout's 4*spp per
 // slot once there are >= 64 slots), the global-memory variant beyond.
 int launch_latin(nart_ctx* ctx, const RenderArgs& ra, hipStream_t st) {
+    // (k_latin_idx at <= 256 spp measured slower: C3 11.0 vs 6.6 ms)
     if (ra.spp <= 256) {
         size_t lds = (size_t)ra.spp * 2 * 64 * sizeof(float);
         hipLaunchKernelGGL(k_latin_lds, dim3((ra.n_slots + 63) / 64), dim3(64), lds, st, ra);
