@@ -108,8 +108,9 @@ struct DScene {
     const BVHNode* nodes;
     const float4* tri_isect;
     // tri_isect's vertices pre-permuted per ray major axis (Triangle::Intersect's
-    // (kx, ky, kz) = (m+1, m+2, m) mod 3, geometry.cpp:48-56): [major][leaf-order tri] 48 B =
-    // {v0p.xyz, v1p.x}, {v1p.yz, v2p.xy}, {v2p.z, global index, info, grazing threshold}
+    // (kx, ky, kz) = (m+1, m+2, m) mod 3, geometry.cpp:48-56): [major][leaf-order tri] 64 B =
+    // {v0p.xyz, v1p.x}, {v1p.yz, v2p.xy}, {v2p.z, global index, info, grazing threshold},
+    // {n, dot(v0, n)} (tri_isect words 0-3)
     const float4* tri_perm;
     const nart_triangle* tris;
     const uint32_t* tri_mesh;

@@ -105,7 +105,31 @@ struct RenderArgs {
     uint32_t rq_quorum = 8;   // k_render_rq: leave a traversal phase once the wave's queue is empty
                               // and at most this many lanes still trace
     const uint32_t* prim = nullptr;  // k_render_rq: camera-ray hits from k_primary, same indexing as samples
+    // k_render_rq: queue entries with bit 31 set are priority pixels (the costliest of a small
+    // shard): their rays are traced first and the traversal phase ends as soon as they resolve
+    uint32_t rq_prio = 0;
+    // k_render_rq: entries with bit 30 set too are pixels dealt to two adjacent lanes, which run
+    // the pixel's sample chain with RNG speculation (see k_render_rq); the queue then holds
+    // qlen entries (the first round's pixels twice), not n_slots
+    uint32_t rq_pairs = 0;
+    uint32_t qlen = 0;
+    // k_render_rq, persistent grid without a queue: a wave whose 64 pixels are all done takes
+    // the next wave-sized group of slots (64 * atomicAdd(ghead, 1)), so waves do not idle until
+    // the other waves of their block end
+    uint32_t* ghead = nullptr;
 };
+#define RQ_PRIO_BIT 0x80000000u
+#define RQ_PAIR_BIT 0x40000000u
+
+// xorshift32 state after n draws (rng.h:38-40 applied n times)
+ND uint32_t rng_jump(uint32_t y, uint32_t n) {
+    for (uint32_t i = 0; i < n; ++i) {
+        y ^= (y << 13);
+        y ^= (y >> 17);
+        y ^= (y << 5);
+    }
+    return y;
+}
 
 ND size_t sample_index(const RenderArgs& A, uint32_t slot, uint32_t s) {
     const SlotSO so = A.slot_so[slot];
@@ -731,12 +755,35 @@ __global__ __launch_bounds__(256) void k_primary(DScene S, RenderArgs A, uint32_
 // next hit.  Each lane's operations and their order are those of k_render (bit-identical).
 //
 // LDS per wave: outbox [kind][lane] 32 B {o, tmax}, {d, -} (kind 0 continuation / camera
-// ray, 1 and 2 the shadow rays), results [lane] {ext hit, shadow 1, shadow 2}, and the
-// list of queued (lane, kind) ids of the current traversal phase.
+// ray, 1 and 2 the shadow rays), results [lane] {ext hit, shadow 1, shadow 2}, and two rings
+// of queued (lane, kind) ids: priority lanes' rays and the others.  A wave has at most 192 rays
+// outstanding (three per lane), so 256-entry rings with 8-bit wrap never overflow.
+//
+// Priority lanes (small shards, RenderArgs::rq_prio): the costliest pixels' serial sample
+// chains set a small shard's time, and in a full wave each of their bounces waited for every
+// queued ray of the wave (~3 traversals per lane) before the next path phase.  Their rays are
+// taken first, and the traversal phase ends once no priority ray is queued or in flight while a
+// priority lane waits for its results; the other lanes' rays stay queued or keep their
+// traversal state for the next phase.  Only the order of work changes (bit-identical).
+//
+// Speculative pairs (RenderArgs::rq_pairs, small shards): a pixel's samples form one chain only
+// through its RNG stream -- sample k+1 starts from the xorshift state sample k ends with -- and the
+// number of draws a sample takes is highly predictable (glassSphere: 76-91 % of a costly pixel's
+// samples take exactly 46 draws, 5 bounces).  A costly pixel therefore gets two lanes: one runs
+// the chain's frontier sample F from its true start state, the other runs sample F+1 from the
+// state F would end with if it took the predicted number of draws (Boyer-Moore majority of the
+// pixel's counts so far).  When F ends, its end state is F+1's true start: if it equals the
+// speculative start, F+1's work is kept (a sample's result depends only on the pixel, the sample
+// index and the start state, so it is exactly the chain's result); otherwise it is dropped and
+// F+1 runs again from the true state.  Results are written only once verified.  Up to two
+// samples per chain step instead of one for the costliest pixels, whose chains bound a small
+// shard; the frame is unchanged (bit-identical).
 #define RQ_PENDING 0xFFFFFFFEu
+#define RQ_RING 256u
 NHD size_t rq_lds_bytes(uint32_t stack_depth, uint32_t block) {
     const uint32_t waves = block / 64;
-    return (size_t)stack_depth * block * 8 + (size_t)waves * 3 * 64 * 32 + (size_t)block * 16 + (size_t)waves * 192;
+    return (size_t)stack_depth * block * 8 + (size_t)waves * 3 * 64 * 32 + (size_t)block * 16 +
+           (size_t)waves * 2 * RQ_RING;
 }
 
 #ifndef NART_RQ_BLOCK
@@ -752,8 +799,9 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
     int2* s_stack = reinterpret_cast<int2*>(s_dyn);
     float4* s_out = reinterpret_cast<float4*>(s_stack + A.stack_depth * blockDim.x);  // [wave][kind][lane][2]
     uint4* s_res = reinterpret_cast<uint4*>(s_out + nwave * 3 * 64 * 2);             // [wave*64 + lane]
-    uint8_t* s_list = reinterpret_cast<uint8_t*>(s_res + blockDim.x) + wv * 192;      // this wave's id list
-    float4* s_nodes = reinterpret_cast<float4*>(reinterpret_cast<uint8_t*>(s_res + blockDim.x) + nwave * 192);
+    uint8_t* s_nring = reinterpret_cast<uint8_t*>(s_res + blockDim.x) + wv * 2 * RQ_RING;  // this wave's id rings
+    uint8_t* s_pring = s_nring + RQ_RING;
+    float4* s_nodes = reinterpret_cast<float4*>(reinterpret_cast<uint8_t*>(s_res + blockDim.x) + nwave * 2 * RQ_RING);
     stage_nodes(S, s_nodes, A.lds_nodes);
     const int nl = (int)A.lds_nodes;
     float4* my_out = s_out + (size_t)wv * 3 * 64 * 2;  // kind k, lane l: my_out[(k * 64 + l) * 2]
@@ -763,11 +811,35 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
     const uint32_t gid = blockIdx.x * blockDim.x + tid;
 
     uint32_t slot = gid;
-    if (A.queue) slot = gid < A.n_slots ? A.queue[gid] : 0xFFFFFFFFu;
-    else if (slot >= A.n_slots) slot = 0xFFFFFFFFu;  // the lane still serves its wave's queue
+    bool gdone = false;  // ghead: no slot group left
+    if (A.ghead) {
+        uint32_t g = 0;
+        if (lane == 0) g = atomicAdd(A.ghead, 1u);
+        g = __builtin_amdgcn_readfirstlane(g);
+        slot = 64u * g + (uint32_t)lane;
+        gdone = 64u * g >= A.n_slots;
+        if (slot >= A.n_slots) slot = 0xFFFFFFFFu;
+    } else if (A.queue) {
+        slot = gid < (A.qlen ? A.qlen : A.n_slots) ? A.queue[gid] : 0xFFFFFFFFu;
+    } else if (slot >= A.n_slots) {
+        slot = 0xFFFFFFFFu;  // the lane still serves its wave's queue
+    }
     uint32_t px = 0, py = 0, rng = 0, sstr = 0;
     uint64_t soff = 0;
+    bool prio = false;  // this lane's pixel is a priority pixel (queue entry bit 31)
+    // speculative pair state (rq_pairs): pm = the lane is one of its pixel's two lanes; the job is
+    // sample s (A.spp: none) from start state jst, verified (start known true) or speculative,
+    // finished (result jres held until verified, end state jend, nd draws) or doomed (dropped
+    // while its rays are still in flight).  pF / pR: the chain frontier (first sample not yet
+    // written) and its true start state; bm: majority vote over the draw counts (val | cnt << 16).
+    bool pm = false;
+    uint32_t jfl = 0, jst = 0, jend = 0, nd = 0, pF = 0, pR = 0, bm = 0;
+    float4 jres = make_float4(0.f, 0.f, 0.f, 0.f);
+    enum { J_VER = 1, J_FIN = 2, J_DOOM = 4 };
     auto take_pixel = [&](uint32_t sl) {
+        prio = A.rq_prio && (sl & RQ_PRIO_BIT);
+        pm = A.rq_pairs && (sl & RQ_PAIR_BIT);
+        if (A.rq_prio) sl &= ~(RQ_PRIO_BIT | RQ_PAIR_BIT);
         slot = sl;
         const uint32_t xy = A.slot_xy[sl];
         px = xy & 0xFFFFu;
@@ -779,6 +851,18 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
     };
     if (slot != 0xFFFFFFFFu) take_pixel(slot);
     uint32_t s = slot != 0xFFFFFFFFu ? 0u : A.spp;
+    if (pm) {
+        // the even lane starts the chain (verified); the odd lane joins once a draw count is known
+        pF = 0;
+        pR = rng;
+        bm = 0;
+        jst = rng;
+        jfl = J_VER;
+        if (lane & 1) {
+            s = A.spp;
+            jfl = 0;
+        }
+    }
 
     TraceCounters cnt = {0u, 0u, 0u, 0u};
     uint32_t n_ext = 0, n_sh = 0, n_bounce = 0;
@@ -797,9 +881,13 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
     Ray tr;
     uint32_t tid8 = 0;  // queued id: owner lane | kind << 6
     bool tracing = false;
+    bool tr_prio = false;  // the ray being traced is a priority lane's
+    // wave-uniform ring positions (ids at [pos & (RQ_RING - 1)]): other / priority rays
+    uint32_t nh = 0, nt = 0, ph = 0, pt = 0;
 
 #ifdef NART_WAVEPROF
     const uint64_t prof_t0 = __builtin_amdgcn_s_memtime();
+    const uint64_t prof_rt0 = __builtin_amdgcn_s_memrealtime();
     uint64_t prof_sec[4] = {0, 0, 0, 0};  // path phase: results + shading, refill, new samples, id lists
     uint64_t prof_last = prof_t0;
     uint32_t prof_shn = 0, prof_sht = 0;  // node visits / triangle tests of shadow rays
@@ -836,6 +924,21 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
         }
         return lightTMax;
     };
+    auto draw = [&]() {
+        ++nd;
+        return rng_float(rng);
+    };
+    // a sample's result: written at once, or held by a pair lane until verified
+    auto end_sample = [&](float4 v) {
+        if (pm) {
+            jres = v;
+            jend = rng;
+            jfl |= J_FIN;
+        } else {
+            A.Lout[soff + (uint64_t)s * sstr] = v;
+            ++s;
+        }
+    };
     auto queue_ext = [&](f3 o, f3 d) {
         put_ray(0, o, d, light_loop(o, d));
         ext_pending = true;
@@ -859,6 +962,9 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
             const uint4 r = *my_res;
             if ((!ext_pending || r.x != RQ_PENDING) && (!use1 || r.y != 2u) && (!use2 || r.z != 2u)) {
                 waiting = false;
+                if (jfl & J_DOOM) {
+                    jfl = 0;  // a dropped speculative job: its rays are back, nothing to keep
+                } else {
                 // L += EstimateDirect(...) * beta, EstimateDirect = ((0 + c1) + c2) * numLights
                 if (have_ed) {
                     f3 Led = F3(0.f, 0.f, 0.f);
@@ -872,15 +978,98 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                 } else {
                     // escaped (at bounce 0 the light seen directly is the result, Q6, Q7) or ended
                     if (ext_pending && bounce == 0 && lightHit) L = Le;
-                    A.Lout[soff + (uint64_t)s * sstr] = make_float4(L.x, L.y, L.z, alpha);
-                    ++s;
+                    end_sample(make_float4(L.x, L.y, L.z, alpha));
                 }
+                }
+            }
+        }
+        // speculative pairs: commit verified results in sample order, check speculative starts,
+        // hand out the next jobs.  Both lanes of a pair evaluate the same function of the pair's
+        // two job records (exchanged with lane ^ 1) and keep their own half.
+        if (A.rq_pairs) {
+            const uint32_t o_s = __shfl_xor(s, 1), o_st = __shfl_xor(jst, 1), o_fl = __shfl_xor(jfl, 1);
+            const uint32_t o_end = __shfl_xor(jend, 1), o_nd = __shfl_xor(nd, 1);
+            const uint32_t o_w = __shfl_xor(waiting ? 1u : 0u, 1);
+            if (pm) {
+                const uint32_t NONE = A.spp;
+                // my job record and my partner's (scalars: no dynamically indexed arrays)
+                uint32_t ms = s, mst = jst, mfl = jfl, os = o_s, ost = o_st, ofl = o_fl;
+                bool mchg = false, ochg = false;  // job dropped or handed out in this step
+#pragma unroll
+                for (int it = 0; it < 2; ++it) {
+                    const bool cm = ms == pF && (mfl & J_VER) && (mfl & J_FIN);
+                    const bool co = os == pF && (ofl & J_VER) && (ofl & J_FIN);
+                    if (!cm && !co) break;
+                    if (cm) A.Lout[soff + (uint64_t)pF * sstr] = jres;
+                    // majority vote over the committed samples' draw counts
+                    const uint32_t n = cm ? nd : o_nd, bv = bm & 0xFFFFu, bc = bm >> 16;
+                    bm = (n == bv) ? (bv | ((bc + 1u) << 16)) : (bc == 0u ? (n | (1u << 16)) : (bv | ((bc - 1u) << 16)));
+                    pR = cm ? jend : o_end;
+                    ++pF;
+                    // the other job is the new frontier's: keep it iff it started from the true state
+                    if (cm) {
+                        ms = NONE;
+                        mfl = 0;
+                        if (os == pF && !(ofl & J_VER)) {
+                            if (ost == pR) {
+                                ofl |= J_VER;
+                            } else {
+                                ofl = o_w ? J_DOOM : 0u;
+                                os = NONE;
+                                ochg = true;
+                            }
+                        }
+                    } else {
+                        os = NONE;
+                        ofl = 0;
+                        if (ms == pF && !(mfl & J_VER)) {
+                            if (mst == pR) {
+                                mfl |= J_VER;
+                            } else {
+                                mfl = waiting ? J_DOOM : 0u;
+                                ms = NONE;
+                                mchg = true;
+                            }
+                        }
+                    }
+                }
+                // next jobs (the even lane first): the frontier from its true state, else the
+                // sample after it from the predicted state (once a draw count has been seen)
+                auto hand_out = [&](uint32_t& xs, uint32_t& xst, uint32_t& xfl, bool& xchg, uint32_t ys) {
+                    if (xs != NONE || (xfl & J_DOOM)) return;
+                    if (pF < A.spp && ys != pF) {
+                        xs = pF;
+                        xst = pR;
+                        xfl = J_VER;
+                        xchg = true;
+                    } else if (pF + 1u < A.spp && ys == pF && (bm >> 16) != 0u) {
+                        xs = pF + 1u;
+                        xst = rng_jump(pR, bm & 0xFFFFu);
+                        xfl = 0;
+                        xchg = true;
+                    }
+                };
+                if ((lane & 1) == 0) {
+                    hand_out(ms, mst, mfl, mchg, os);
+                    hand_out(os, ost, ofl, ochg, ms);
+                } else {
+                    hand_out(os, ost, ofl, ochg, ms);
+                    hand_out(ms, mst, mfl, mchg, os);
+                }
+                if (mchg) {
+                    need_shade = false;  // a dropped job's pending hit, or a job that starts afresh
+                    rng = mst;
+                }
+                s = ms;
+                jst = mst;
+                jfl = mfl;
+                if (pF >= A.spp && ms == NONE && os == NONE && !((mfl | ofl) & J_DOOM)) pm = false;
             }
         }
         RQ_MARK(0);
         // pixel refill (persistent grid): one queue atomic per wave
         if (A.qhead) {
-            const bool need = !waiting && s >= A.spp && slot != 0xFFFFFFFEu;
+            const bool need = !pm && !waiting && s >= A.spp && slot != 0xFFFFFFFEu;
             const uint64_t m = __ballot(need);
             if (m) {
                 const int leader = __builtin_ctzll(m);
@@ -890,7 +1079,7 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                 if (need) {
                     const uint32_t idx = A.qbase + base +
                         __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    if (idx < A.n_slots) {
+                    if (idx < (A.qlen ? A.qlen : A.n_slots)) {
                         take_pixel(A.queue[idx]);
                         s = 0;
                     } else {
@@ -899,12 +1088,25 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                 }
             }
         }
-        bool active = !waiting && !need_shade && s < A.spp;
+        if (A.ghead && !gdone && __ballot(waiting || need_shade || tracing || s < A.spp) == 0) {
+            // every pixel of the wave is done: the next group of 64 slots (one atomic per wave)
+            uint32_t g = 0;
+            if (lane == 0) g = atomicAdd(A.ghead, 1u);
+            g = __builtin_amdgcn_readfirstlane(g);
+            gdone = 64u * g >= A.n_slots;
+            const uint32_t sl = 64u * g + (uint32_t)lane;
+            if (sl < A.n_slots) {
+                take_pixel(sl);
+                s = 0;
+            }
+        }
+        bool active = !waiting && !need_shade && s < A.spp && !(jfl & J_FIN);
         RQ_MARK(1);
         // 2. new samples (pathintegrator.cpp:144-166; render.cpp:87-95).  A camera ray that
         //    k_primary found to escape, or a zero bounce limit, ends its sample here, so loop until
         //    a hit is to be shaded, a ray is queued or the pixel is done.
         while (active) {
+            nd = 0;
             const float2 sm = A.samples[soff + (uint64_t)s * sstr];
             const Ray ray = cast_ray(S, F2(sm.x, sm.y), A.W, A.H, px, py);
             L = F3(0.f, 0.f, 0.f);
@@ -919,9 +1121,8 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
             use1 = use2 = have_ed = false;
             ext_pending = false;
             if (A.bounces == 0) {
-                A.Lout[soff + (uint64_t)s * sstr] = make_float4(0.f, 0.f, 0.f, 0.f);
-                ++s;
-                active = s < A.spp;
+                end_sample(make_float4(0.f, 0.f, 0.f, 0.f));
+                active = !pm && s < A.spp;
                 continue;
             }
             if (A.prim) {
@@ -930,9 +1131,8 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                 const uint32_t g = A.prim[soff + (uint64_t)s * sstr];
                 if (g == NO_HIT) {
                     if (lightHit) L = Le;
-                    A.Lout[soff + (uint64_t)s * sstr] = make_float4(L.x, L.y, L.z, alpha);
-                    ++s;
-                    active = s < A.spp;
+                    end_sample(make_float4(L.x, L.y, L.z, alpha));
+                    active = !pm && s < A.spp;
                     continue;
                 }
                 float4* e = my_out + lane * 2;
@@ -964,11 +1164,11 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                 if (bounce == 0) alpha = 1.f;
                 const f3 wo = to_local(bsdf, neg(cur.d));
                 // ---- EstimateDirect (pathintegrator.cpp:38-121)
-                const DLight& Lg = S.lights[f2u8(gmin(rng_float(rng), ND_ONE_MINUS_EPS) * nL)];
+                const DLight& Lg = S.lights[f2u8(gmin(draw(), ND_ONE_MINUS_EPS) * nL)];
                 float sPdf = 0.f, lPdf = 0.f;
-                float sx = rng_float(rng);
-                float sy = rng_float(rng);
-                float bsmp = rng_float(rng);
+                float sx = draw();
+                float sy = draw();
+                float bsmp = draw();
                 uint32_t dflags = 0;
                 f3 wi;
                 f3 f = bsdf_sample_f(bsdf, wo, wi, bsmp, F2(sx, sy), sPdf, dflags, true, eta_outer, nullptr,
@@ -992,8 +1192,8 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                     }
                 }
                 lPdf = 0.f;
-                float lx = rng_float(rng);
-                float ly = rng_float(rng);
+                float lx = draw();
+                float ly = draw();
                 f3 wiW;
                 float lt2 = __builtin_inff();
                 f3 Li2 = light_sample_li<ENV>(S, Lg, is.p, wiW, F2(lx, ly), lPdf, lt2);
@@ -1014,9 +1214,9 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                 betak = beta;
                 have_ed = true;
                 // ---- continuation (pathintegrator.cpp:199-220)
-                float a = rng_float(rng);
-                float b = rng_float(rng);
-                float bs2 = rng_float(rng);
+                float a = draw();
+                float b = draw();
+                float bs2 = draw();
                 float cpdf = 0.f, alpha_i = 0.f;
                 f3 wic;
                 f3 fc = bsdf_sample_f(bsdf, wo, wic, bs2, F2(a, b), cpdf, flags, false, eta_outer, &alpha_i,
@@ -1036,7 +1236,7 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                 no = add(is.p, muls(cur.d, SHADOW_BIAS));
                 nd = cur.d;
                 flags = F_TRANSMISSIVE;
-                float bs2 = rng_float(rng);
+                float bs2 = draw();
                 eta_sampled = bsdf_sample_eta(bsdf, bs2);
                 cont = true;
                 have_ed = false;
@@ -1046,7 +1246,7 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                 // Russian roulette (pathintegrator.cpp:236-246)
                 float q = gmax((beta.x + beta.y + beta.z) * 0.33333f, 0.f);
                 if (bounce > 3) {
-                    if (q >= rng_float(rng)) beta = divs(beta, q);
+                    if (q >= draw()) beta = divs(beta, q);
                     else cont = false;
                 }
             }
@@ -1060,8 +1260,7 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                 // no query left (path ended, or ended at the bounce limit): the EstimateDirect
                 // term of this bounce, if any, is still owed
                 if (have_ed) L = add(L, mul(muls(F3(0.f, 0.f, 0.f), nL), betak));
-                A.Lout[soff + (uint64_t)s * sstr] = make_float4(L.x, L.y, L.z, alpha);
-                ++s;
+                end_sample(make_float4(L.x, L.y, L.z, alpha));
             }
         }
         // queued rays: init the result words, then list the (lane, kind) ids in kind order
@@ -1072,45 +1271,58 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
             if (newk & 4u) r0.z = 2u;
             *my_res = r0;
         }
-        uint32_t nq = 0;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const bool want = (newk >> k) & 1u;
-            const uint64_t m = __ballot(want);
-            if (want) {
+            const bool wp = want && prio, wn = want && !prio;
+            const uint64_t m = __ballot(wn);
+            if (wn) {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                s_list[nq + rank] = (uint8_t)(lane | (k << 6));
+                s_nring[(nt + rank) & (RQ_RING - 1u)] = (uint8_t)(lane | (k << 6));
             }
-            nq += (uint32_t)__popcll(m);
+            nt += (uint32_t)__popcll(m);
+            if (A.rq_prio) {
+                const uint64_t mp = __ballot(wp);
+                if (wp) {
+                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mp >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mp, 0u));
+                    s_pring[(pt + rank) & (RQ_RING - 1u)] = (uint8_t)(lane | (k << 6));
+                }
+                pt += (uint32_t)__popcll(mp);
+            }
         }
         RQ_MARK(3);
         // a lane whose sample ended while shading starts its next sample in the next phase; one
         // whose pixel is done may still get a pixel from the queue
-        const bool more = !waiting && (s < A.spp || (A.qhead && slot != 0xFFFFFFFEu));
+        const bool more = !waiting && (s < A.spp || pm || (A.qhead && slot != 0xFFFFFFFEu) || (A.ghead && !gdone));
         if (__ballot(waiting || tracing || more) == 0) break;  // every path of the wave is done
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
         // ---------------- traversal phase: lanes take the wave's queued rays in turn
-        uint32_t head = 0;
 #ifdef NART_WAVEPROF
         const uint64_t prof_tt = __builtin_amdgcn_s_memtime();
 #endif
         for (;;) {
             const bool need = !tracing;
             const uint64_t mn = __ballot(need);
-            if (mn && head < nq) {
+            const uint32_t avp = pt - ph, avn = nt - nh;
+            if (mn && avp + avn > 0u) {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mn >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)mn, 0u));
-                if (need && head + rank < nq) {
-                    tid8 = s_list[head + rank];
+                if (need && rank < avp + avn) {
+                    tr_prio = rank < avp;
+                    tid8 = tr_prio ? s_pring[(ph + rank) & (RQ_RING - 1u)] : s_nring[(nh + rank - avp) & (RQ_RING - 1u)];
                     const uint32_t owner = tid8 & 63u, kind = tid8 >> 6;
                     const float4 a = my_out[(kind * 64 + owner) * 2], b = my_out[(kind * 64 + owner) * 2 + 1];
                     tr = make_ray(F3(a.x, a.y, a.z), F3(b.x, b.y, b.z));
                     trav_begin(S, tr, a.w, kind != 0u, tq);
                     tracing = true;
                 }
-                head += min((uint32_t)__popcll(mn), nq - head);
+                const uint32_t took = min((uint32_t)__popcll(mn), avp + avn);
+                const uint32_t tp = min(took, avp);
+                ph += tp;
+                nh += took - tp;
             }
             bool fin = false;
             if (tracing) {
@@ -1135,13 +1347,21 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                 const uint32_t kind = tid8 >> 6;
                 rw[kind] = kind == 0u ? bg : (bg != NO_HIT ? 1u : 0u);
             }
-            if (head >= nq && (uint32_t)__popcll(__ballot(tracing)) <= A.rq_quorum) break;
+            // priority rays all resolved and a priority lane waits on its results: shade it now
+            if (A.rq_prio && ph == pt && __ballot(tracing && tr_prio) == 0 && __ballot(waiting && prio) != 0) break;
+            if (ph == pt && nh == nt && (uint32_t)__popcll(__ballot(tracing)) <= A.rq_quorum) break;
         }
 #ifdef NART_WAVEPROF
         if (COUNT && (int)__lane_id() == __builtin_ctzll(__ballot(1))) cnt.pw[6] += __builtin_amdgcn_s_memtime() - prof_tt;
 #endif
     }
 #ifdef NART_WAVEPROF
+    if (COUNT && lane == 0) {
+        // wave timeline (constant-rate global clock): start, end
+        unsigned long long* wvr = A.counters + 24 + 8 * 70000 + 4200000 - 2 * 70000 + 2 * (size_t)(gid / 64);
+        wvr[0] = prof_rt0;
+        wvr[1] = __builtin_amdgcn_s_memrealtime();
+    }
     if (COUNT) {
         if (lane == 0) cnt.pw[7] += __builtin_amdgcn_s_memtime() - prof_t0;
         for (int i = 0; i < 12; ++i) atomicAdd(&A.counters[8 + i], (unsigned long long)cnt.pw[i]);

@@ -229,7 +229,16 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
         bool h0 = (n0 <= f0) && (f0 >= 0.f) && (n0 <= t.cullT);
         bool h1 = (n1 <= f1) && (f1 >= 0.f) && (n1 <= t.cullT);
         if (h0 && h1) {
+#if defined(NART_ORDER) && NART_ORDER == 1
+            // entry distances clamped to the origin; ties (both boxes hold the origin) by exit
+            const float k0 = fmaxf(n0, 0.f), k1 = fmaxf(n1, 0.f);
+            bool swap = k1 < k0 || (k1 == k0 && f1 < f0);
+#elif defined(NART_ORDER) && NART_ORDER == 2
+            const float k0 = fmaxf(n0, 0.f), k1 = fmaxf(n1, 0.f);
+            bool swap = k1 < k0 || (k1 == k0 && f1 > f0);
+#else
             bool swap = n1 < n0;
+#endif
             stk_push(sc, st, stride, t.sp, swap ? k.x : k.y, swap ? n0 : n1);
             ++t.sp;
             t.code = swap ? k.y : k.x;
@@ -245,14 +254,15 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
     const uint32_t first = lc >> 5, count = (lc & 31u) + 1u;
     // Vertices pre-permuted for this ray's major axis (DScene::tri_perm): v - o in permuted
     // order is (vp - op) component by component, the same subtractions as geometry.cpp:42-56,
-    // without 18 per-triangle selects (C3 at 64 spp: 134.9 -> 133.3 ms).  The plane record
-    // {n, dot(v0, n)} is read only for triangles whose edge test passes.
+    // without 18 per-triangle selects (C3 at 64 spp: 134.9 -> 133.3 ms).
     const f3 op = permute(r.o, r.major);
-    const float4* tpp = S.tri_perm + 3 * ((size_t)r.major * S.num_leaf_tris + first);
+    const float4* tpp = S.tri_perm + 4 * ((size_t)r.major * S.num_leaf_tris + first);
     for (uint32_t i = 0; i < count; ++i) {
         if (COUNT) cnt.tris++;
         if (COUNT) WPROF(cnt, 4);
-        const float4 b = tpp[3 * i], c = tpp[3 * i + 1], dd = tpp[3 * i + 2];
+        // the plane is loaded with the vertices (same 64-B record), not after the edge test:
+        // one memory round trip per test instead of two
+        const float4 b = tpp[4 * i], c = tpp[4 * i + 1], dd = tpp[4 * i + 2], a = tpp[4 * i + 3];
         f3 p0 = F3(b.x - op.x, b.y - op.y, b.z - op.z);
         f3 p1 = F3(b.w - op.x, c.x - op.y, c.y - op.z);
         f3 p2 = F3(c.z - op.x, c.w - op.y, dd.x - op.z);
@@ -266,7 +276,6 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
         const float e1 = (p2.x * p0.y) - (p2.y * p0.x);
         const float e2 = (p0.x * p1.y) - (p0.y * p1.x);
         if (!edges_accept(e0, e1, e2)) continue;
-        const float4 a = S.tri_isect[4 * (first + i)];
         f3 n = F3(a.x, a.y, a.z);
         const float den = dot(r.d, n);
         float tt = (a.w - dot(r.o, n)) / den;

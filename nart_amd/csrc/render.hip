@@ -416,16 +416,20 @@ __global__ void k_flag_top(const uint32_t* sorted, uint32_t n, uint32_t E, uint3
 // Queue: in the first round of W waves, lanes j < k of wave w take the costly pixel of rank
 // j*W + w (each wave holds k of them); every other position takes the remaining pixels in
 // slot order (spatially coherent waves).
+// With prio set (k_render_rq) the costly entries carry RQ_PRIO_BIT; with pairs each costly pixel
+// goes to two adjacent lanes (2j, 2j + 1) with RQ_PAIR_BIT too, and the queue is n + k*W long.
 __global__ void k_build_queue(const uint32_t* top, const uint32_t* rest, uint32_t n, uint32_t W, uint32_t k,
-                              uint32_t* queue) {
+                              uint32_t prio, uint32_t pairs, uint32_t* queue) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n) return;
+    const uint32_t per = pairs ? 2u : 1u, kk = per * k;  // first-round lanes of the costly pixels
+    if (p >= n + (pairs ? k * W : 0u)) return;
     const uint32_t g = 64u * W;
     if (p < g) {
         const uint32_t w = p / 64u, j = p % 64u;
-        queue[p] = j < k ? top[j * W + w] : rest[w * (64u - k) + (j - k)];
+        queue[p] = j < kk ? (top[(j / per) * W + w] | prio | (pairs ? RQ_PAIR_BIT : 0u))
+                          : rest[w * (64u - kk) + (j - kk)];
     } else {
-        queue[p] = rest[(64u - k) * W + (p - g)];
+        queue[p] = rest[(64u - kk) * W + (p - g)];
     }
 }
 
@@ -544,7 +548,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     if (mode > 0) {
         if (blocks > resident) {  // more pixels than resident lanes: persistent grid + queue
             const uint32_t n = a.n_slots;
-            int rc = ensure_queue(ctx, n);
+            int rc = ensure_queue(ctx, n + 32u * W);  // room for the speculative pairs' duplicates
             if (rc) return rc;
             const dim3 eg((n + 255) / 256);
             // costly pixels per first-round wave: few when the shard is small (their serial chains
@@ -552,7 +556,19 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             uint32_t k = R >= 3.0 ? 32u : 8u;  // measured on C3 shards of 1/2, 1/4, 1/8 of the frame
             if (R >= 12.0 && mode == 2 && !std::getenv("NART_QUEUE_K")) {
                 // many rounds: the slot order (costly waves interleaved with cheap ones in time)
-                // measured faster than any reordering; no probe
+                // measured faster than any reordering; no probe.  The ray-queue kernel runs it on
+                // a persistent grid whose waves take wave-sized slot groups in that order
+                // (NART_RQ_GROUPS=0: one wave per group, blocks retiring as a whole)
+                const bool groups = rq && (!std::getenv("NART_RQ_GROUPS") || std::atoi(std::getenv("NART_RQ_GROUPS")) != 0);
+                if (groups) {
+                    int per_cu_rq = 0;
+                    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_rq, (const void*)kern_rq, NART_RQ_BLOCK,
+                                                                       lds_rq));
+                    HIPCHK(hipMemsetAsync(ctx->d_qhead, 0, sizeof(uint32_t), st));
+                    b.ghead = ctx->d_qhead;
+                    // launches are counted in blocks of 256 threads
+                    blocks = std::min(blocks, (uint32_t)std::max(1, cus * std::max(per_cu_rq, 1)) * (NART_RQ_BLOCK / 256));
+                }
                 launch(blocks, b);
                 HIPCHK(hipGetLastError());
                 return NART_OK;
@@ -582,8 +598,18 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                 tmp = ctx->cap_sort_tmp;
                 HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->d_sort_tmp, tmp, ctx->d_keys[0], ctx->d_keys[1],
                                                           ctx->d_cost, ctx->d_vals[0], (int)n, 0, 1, st));
-                hipLaunchKernelGGL(k_build_queue, eg, block, 0, st, ctx->d_vals[1], ctx->d_vals[0], n, W, k,
-                                   ctx->d_queue);
+                // priority lanes for the costly pixels in the ray-queue kernel (NART_RQ_PRIO=0: off),
+                // run as speculative lane pairs (NART_RQ_PAIRS=0: one lane per pixel)
+                static const bool prio_on = !std::getenv("NART_RQ_PRIO") || std::atoi(std::getenv("NART_RQ_PRIO")) != 0;
+                const bool pairs_on = !std::getenv("NART_RQ_PAIRS") || std::atoi(std::getenv("NART_RQ_PAIRS")) != 0;
+                const uint32_t pbit = (rq && prio_on) ? RQ_PRIO_BIT : 0u;
+                const bool pairs = pbit && pairs_on && 2u * k <= 64u;
+                const uint32_t qlen = n + (pairs ? k * W : 0u);
+                hipLaunchKernelGGL(k_build_queue, dim3((qlen + 255) / 256), block, 0, st, ctx->d_vals[1], ctx->d_vals[0],
+                                   n, W, k, pbit, pairs ? 1u : 0u, ctx->d_queue);
+                b.rq_prio = pbit ? 1u : 0u;
+                b.rq_pairs = pairs ? 1u : 0u;
+                b.qlen = qlen;
             }
             b.queue = ctx->d_queue;
             if (refill) {
@@ -1039,6 +1065,33 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
                             pw[8 * i + 1], pw[8 * i + 2], pw[8 * i + 4], pw[8 * i + 5], pw[8 * i + 6], pw[8 * i + 7], s0 < xy.size() ? xy[s0] & 0xFFFF : 0, s0 < xy.size() ? xy[s0] >> 16 : 0);
                 }
             }
+            {
+                // ray-queue kernel wave timeline (s_memrealtime, 100 MHz): waves still running at
+                // fractions of the launch span
+                const uint32_t nw = (uint32_t)std::min<size_t>((xy.size() + 63) / 64, 70000);
+                std::vector<unsigned long long> pw(2 * (size_t)nw);
+                HIPCHK(hipMemcpy(pw.data(), ctx->d_counters + 24 + 8 * 70000 + 4200000 - 2 * 70000, pw.size() * 8,
+                                 hipMemcpyDeviceToHost));
+                unsigned long long t0 = ~0ull, t1 = 0;
+                uint32_t nv = 0;
+                for (uint32_t i = 0; i < nw; ++i)
+                    if (pw[2 * i + 1]) {
+                        t0 = std::min(t0, pw[2 * i]);
+                        t1 = std::max(t1, pw[2 * i + 1]);
+                        ++nv;
+                    }
+                if (nv) {
+                    fprintf(stderr, "WAVETL waves %u span %.2f ms; running at", nv, (t1 - t0) * 1e-5);
+                    for (double f : {0.1, 0.25, 0.4, 0.5, 0.6, 0.7, 0.8, 0.9, 0.95}) {
+                        const unsigned long long t = t0 + (unsigned long long)(f * (t1 - t0));
+                        uint32_t run = 0;
+                        for (uint32_t i = 0; i < nw; ++i)
+                            if (pw[2 * i + 1] && pw[2 * i] <= t && pw[2 * i + 1] > t) ++run;
+                        fprintf(stderr, " %.0f%%:%u", f * 100, run);
+                    }
+                    fprintf(stderr, "\n");
+                }
+            }
             if (const char* dump = std::getenv("NART_WAVEPROF_DUMP")) {
                 std::vector<unsigned long long> ps(xy.size());
                 HIPCHK(hipMemcpy(ps.data(), ctx->d_counters + 24 + 8 * 70000, ps.size() * 8, hipMemcpyDeviceToHost));
@@ -1126,15 +1179,16 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     ctx->num_nodes = (uint32_t)bvh.nodes.size();
     if ((rc = upload(ctx, ctx->d_tri_isect, bvh.tri_isect.data(), bvh.tri_isect.size()))) return bail(rc);
     {
-        // vertex block of every triangle test record, permuted for each ray major axis
+        // vertex block of every triangle test record, permuted for each ray major axis, followed
+        // by the plane {n, dot(v0, n)}: one 64-B record, so a test issues its four loads at once
         const size_t nt = bvh.tri_isect.size() / 16;
-        std::vector<float> perm(3 * nt * 12);
+        std::vector<float> perm(3 * nt * 16);
         for (int m = 0; m < 3; ++m) {
             const int kx = (m + 1) % 3, ky = (m + 2) % 3, kz = m;
             for (size_t i = 0; i < nt; ++i) {
                 const float* r = &bvh.tri_isect[i * 16];
                 const float* v[3] = {r + 4, r + 7, r + 10};  // v0, v1, v2 (words 4-12)
-                float* o = &perm[((size_t)m * nt + i) * 12];
+                float* o = &perm[((size_t)m * nt + i) * 16];
                 for (int k = 0; k < 3; ++k) {
                     o[3 * k + 0] = v[k][kx];
                     o[3 * k + 1] = v[k][ky];
@@ -1143,6 +1197,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
                 o[9] = r[13];   // global index
                 o[10] = r[14];  // octree leaf | inside bit
                 o[11] = r[15];  // grazing threshold
+                for (int k = 0; k < 4; ++k) o[12 + k] = r[k];  // plane (words 0-3)
             }
         }
         if ((rc = upload(ctx, ctx->d_tri_perm, perm.data(), perm.size()))) return bail(rc);
@@ -1375,7 +1430,13 @@ int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t
     if (rc) return rc;
     HIPCHK(hipMemcpy(ctx->d_slot_xy, xy.data(), (size_t)n * 4, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(k_slot_rows, dim3((n + 255) / 256), dim3(256), 0, 0, n, p->spp, ctx->d_slot_so);
-    if (!ctx->d_counters) HIPCHK(hipMalloc(&ctx->d_counters, 24 * sizeof(unsigned long long)));
+#ifdef NART_WAVEPROF
+    const size_t n_cnt = 24 + 8 * 70000 + 4200000;  // as the bucket path (development profile)
+#else
+    const size_t n_cnt = 24;
+#endif
+    if (!ctx->d_counters) HIPCHK(hipMalloc(&ctx->d_counters, n_cnt * sizeof(unsigned long long)));
+    if (ctx->counters) HIPCHK(hipMemset(ctx->d_counters, 0, n_cnt * sizeof(unsigned long long)));
     RenderArgs ra;
     ra.slot_xy = ctx->d_slot_xy;
     ra.slot_so = ctx->d_slot_so;
@@ -1394,9 +1455,50 @@ int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t
     ra.counters = ctx->d_counters;
     rc = launch_latin(ctx, ra, 0);
     if (rc) return rc;
-    rc = dispatch_render(ctx, ra, p->integrator, 0);
-    if (rc) return rc;
+    if (std::getenv("NART_SAMPLES_PAIRS") && std::atoi(std::getenv("NART_SAMPLES_PAIRS")) && ctx->variant == 0 &&
+        p->integrator == NART_INTEGRATOR_PATH && n <= 65536) {
+        // development probe of the speculative pairs: every pixel of the rect on two lanes
+        // (the ray-queue kernel alone, camera rays included; no work queue refill)
+        rc = ensure_queue(ctx, 2 * n);
+        if (rc) return rc;
+        std::vector<uint32_t> q(2 * n);
+        for (uint32_t i = 0; i < n; ++i) q[2 * i] = q[2 * i + 1] = i | RQ_PRIO_BIT | RQ_PAIR_BIT;
+        HIPCHK(hipMemcpy(ctx->d_queue, q.data(), q.size() * 4, hipMemcpyHostToDevice));
+        RenderArgs r2 = ra;
+        r2.queue = ctx->d_queue;
+        r2.qlen = 2 * n;
+        r2.rq_prio = 1;
+        r2.rq_pairs = 1;
+        r2.rq_quorum = 0;
+        r2.lds_nodes = render_lds_nodes(ctx, rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK), NART_RQ_BLOCK / 256);
+        const size_t lds_rq = rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK) + (size_t)r2.lds_nodes * sizeof(BVHNode);
+        static bool attr = false;
+        auto kern = k_render_rq<10, false, false>;
+        if (!attr) {
+            hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr = true;
+        }
+        if (ctx->has_env || p->bounces > 10) return fail(ctx, NART_E_UNSUPPORTED, "pairs probe: glass-like scenes only");
+        hipLaunchKernelGGL(kern, dim3((2 * n + NART_RQ_BLOCK - 1) / NART_RQ_BLOCK), dim3(NART_RQ_BLOCK), lds_rq, 0,
+                           ctx->scene, r2);
+        HIPCHK(hipGetLastError());
+    } else {
+        rc = dispatch_render(ctx, ra, p->integrator, 0);
+        if (rc) return rc;
+    }
     HIPCHK(hipMemcpy(out, ctx->d_L, (size_t)n * p->spp * sizeof(float4), hipMemcpyDeviceToHost));
+#ifdef NART_WAVEPROF
+    if (ctx->counters) {
+        unsigned long long c[24], sc[8];
+        HIPCHK(hipMemcpy(c, ctx->d_counters, sizeof(c), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(sc, ctx->d_counters + 24 + 8 * 69999, sizeof(sc), hipMemcpyDeviceToHost));
+        fprintf(stderr, "WAVEPROF samples: ext %llu shadow %llu nodes %llu tris %llu bounces %llu\n", c[0], c[1], c[2], c[3], c[4]);
+        fprintf(stderr, "WAVEPROF rq path sections results+shading %llu refill %llu new_samples %llu id_lists %llu shadow nodes %llu tris %llu\n",
+                sc[0], sc[1], sc[2], sc[3], sc[4], sc[5]);
+        fprintf(stderr, "WAVEPROF steps %llu/%llu nodes %llu/%llu tris %llu/%llu trav_cyc %llu total_cyc %llu shade %llu/%llu phases %llu path_cyc %llu\n",
+                c[8], c[9], c[10], c[11], c[12], c[13], c[14], c[15], c[16], c[17], c[18], c[19]);
+    }
+#endif
     return NART_OK;
 }
 

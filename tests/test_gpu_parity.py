@@ -91,12 +91,26 @@ def test_framebuffer_glass_sphere_c1(glass_gpu, glass_oracle, glass_scene):
     assert np.isfinite(res).all()
 
 
-@pytest.mark.parametrize("w,h", [(1024, 576), (512, 400)], ids=["k32", "k8"])
-def test_queue_scheduler_frames(gpu, glass_scene, w, h):
+@pytest.mark.parametrize("w,h,spp", [(1024, 576, 2), (512, 400, 2), (512, 400, 6)], ids=["k32", "k8", "k8-6spp"])
+def test_queue_scheduler_frames(gpu, glass_scene, w, h, spp):
     """More traced pixels than resident lanes: the megakernel runs the cost probe, the costly
     pixels are spread over the persistent waves and finished lanes refill from the queue
-    (render.hip launch_render).  Only the order of work changes; the frame must not."""
-    p = _params(glass_scene, w, h, 2)
+    (render.hip launch_render); in the ray-queue kernel they are priority lanes whose rays are
+    traced first.  Only the order of work changes; the frame must not."""
+    p = _params(glass_scene, w, h, spp)
+    g = nart_amd.HipRenderer(glass_scene, variant=0).render(p)
+    r = oracle.Oracle(glass_scene).render(p)
+    assert _bits_equal(g, r), _report(g, r)
+
+
+@pytest.mark.parametrize("pairs", ["1", "0"], ids=["speculative-pairs", "single-lanes"])
+def test_queue_speculative_pairs(gpu, glass_scene, monkeypatch, pairs):
+    """A shard of ~1.2 rounds of resident waves at 24 spp: the costliest pixels run as speculative
+    lane pairs (one lane on the chain's frontier sample, the other on the next sample from a
+    predicted RNG state; kept only when the prediction was exact).  Long enough chains for both
+    kept and dropped speculation; the frame must equal the oracle's bit for bit."""
+    monkeypatch.setenv("NART_RQ_PAIRS", pairs)
+    p = _params(glass_scene, 512, 300, 24)
     g = nart_amd.HipRenderer(glass_scene, variant=0).render(p)
     r = oracle.Oracle(glass_scene).render(p)
     assert _bits_equal(g, r), _report(g, r)
