@@ -598,9 +598,14 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                 tmp = ctx->cap_sort_tmp;
                 HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->d_sort_tmp, tmp, ctx->d_keys[0], ctx->d_keys[1],
                                                           ctx->d_cost, ctx->d_vals[0], (int)n, 0, 1, st));
-                // priority lanes for the costly pixels in the ray-queue kernel (NART_RQ_PRIO=0: off),
-                // run as speculative lane pairs (NART_RQ_PAIRS=0: one lane per pixel)
-                static const bool prio_on = !std::getenv("NART_RQ_PRIO") || std::atoi(std::getenv("NART_RQ_PRIO")) != 0;
+                // priority lanes for the costly pixels in the ray-queue kernel (NART_RQ_PRIO=0: off,
+                // 2: also on launches of >= 3 rounds), run as speculative lane pairs
+                // (NART_RQ_PAIRS=0: one lane per pixel).  Only small shards (< 3 rounds of
+                // resident waves), whose time is their costliest pixels' chains: on throughput-bound
+                // launches the priority breaks and the speculative duplicates cost throughput
+                // (1/2 C3 shard 238 -> 249 ms, C4 batches 3175 -> 3381 ms with them on)
+                const int prio_env = std::getenv("NART_RQ_PRIO") ? std::atoi(std::getenv("NART_RQ_PRIO")) : 1;
+                const bool prio_on = prio_env == 2 || (prio_env == 1 && R < q_rounds);
                 const bool pairs_on = !std::getenv("NART_RQ_PAIRS") || std::atoi(std::getenv("NART_RQ_PAIRS")) != 0;
                 const uint32_t pbit = (rq && prio_on) ? RQ_PRIO_BIT : 0u;
                 const bool pairs = pbit && pairs_on && 2u * k <= 64u;

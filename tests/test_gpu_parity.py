@@ -91,12 +91,16 @@ def test_framebuffer_glass_sphere_c1(glass_gpu, glass_oracle, glass_scene):
     assert np.isfinite(res).all()
 
 
-@pytest.mark.parametrize("w,h,spp", [(1024, 576, 2), (512, 400, 2), (512, 400, 6)], ids=["k32", "k8", "k8-6spp"])
-def test_queue_scheduler_frames(gpu, glass_scene, w, h, spp):
+@pytest.mark.parametrize("w,h,spp,prio", [(1024, 576, 2, "1"), (1024, 576, 2, "2"), (512, 400, 2, "1"), (512, 400, 6, "1")],
+                         ids=["k32", "k32-prio", "k8", "k8-6spp"])
+def test_queue_scheduler_frames(gpu, glass_scene, monkeypatch, w, h, spp, prio):
     """More traced pixels than resident lanes: the megakernel runs the cost probe, the costly
     pixels are spread over the persistent waves and finished lanes refill from the queue
     (render.hip launch_render); in the ray-queue kernel they are priority lanes whose rays are
-    traced first.  Only the order of work changes; the frame must not."""
+    traced first (small shards; NART_RQ_PRIO=2 forces them on at >= 3 rounds, k32-prio: 32
+    costly pixels per wave as speculative pairs filling whole waves).  Only the order of work
+    changes; the frame must not."""
+    monkeypatch.setenv("NART_RQ_PRIO", prio)
     p = _params(glass_scene, w, h, spp)
     g = nart_amd.HipRenderer(glass_scene, variant=0).render(p)
     r = oracle.Oracle(glass_scene).render(p)
