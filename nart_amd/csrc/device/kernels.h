@@ -117,6 +117,8 @@ struct RenderArgs {
     // the next wave-sized group of slots (64 * atomicAdd(ghead, 1)), so waves do not idle until
     // the other waves of their block end
     uint32_t* ghead = nullptr;
+    // with ghead: the n-th group taken is gorder[n] (null: slot order)
+    const uint32_t* gorder = nullptr;
 };
 #define RQ_PRIO_BIT 0x80000000u
 #define RQ_PAIR_BIT 0x40000000u
@@ -816,9 +818,10 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
         uint32_t g = 0;
         if (lane == 0) g = atomicAdd(A.ghead, 1u);
         g = __builtin_amdgcn_readfirstlane(g);
-        slot = 64u * g + (uint32_t)lane;
         gdone = 64u * g >= A.n_slots;
-        if (slot >= A.n_slots) slot = 0xFFFFFFFFu;
+        if (A.gorder && !gdone) g = A.gorder[g];
+        slot = 64u * g + (uint32_t)lane;
+        if (gdone || slot >= A.n_slots) slot = 0xFFFFFFFFu;
     } else if (A.queue) {
         slot = gid < (A.qlen ? A.qlen : A.n_slots) ? A.queue[gid] : 0xFFFFFFFFu;
     } else if (slot >= A.n_slots) {
@@ -1094,8 +1097,9 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
             if (lane == 0) g = atomicAdd(A.ghead, 1u);
             g = __builtin_amdgcn_readfirstlane(g);
             gdone = 64u * g >= A.n_slots;
+            if (A.gorder && !gdone) g = A.gorder[g];
             const uint32_t sl = 64u * g + (uint32_t)lane;
-            if (sl < A.n_slots) {
+            if (!gdone && sl < A.n_slots) {
                 take_pixel(sl);
                 s = 0;
             }

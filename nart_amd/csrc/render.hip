@@ -399,6 +399,16 @@ __global__ void k_group_keys(const uint32_t* cost, uint32_t n, uint32_t* keys, u
     vals[g] = g;
 }
 
+// Two cost classes of groups for the wave-group refill order: keys[g] = 0 for the E costliest
+// groups (ranks [0, E) of the cost-sorted list), 1 for the rest; vals = group ids in slot order,
+// so a stable sort by the key keeps slot order inside each class.
+__global__ void k_group_class(const uint32_t* sorted, uint32_t ng, uint32_t E, uint32_t* keys, uint32_t* vals) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= ng) return;
+    keys[sorted[r]] = r < E ? 0u : 1u;
+    vals[r] = r;
+}
+
 // Pixel list of the sorted groups (group order, slot order inside a group).
 __global__ void k_expand_groups(const uint32_t* groups, uint32_t n, uint32_t* pixels) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -566,6 +576,38 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                                                                        lds_rq));
                     HIPCHK(hipMemsetAsync(ctx->d_qhead, 0, sizeof(uint32_t), st));
                     b.ghead = ctx->d_qhead;
+                    // group order (NART_RQ_ORDER): 0 slot order; 1 costliest group first (cost
+                    // probe); 2 (default) the NART_RQ_TOPF % (default 10) costliest groups first,
+                    // each class in slot order.  In slot order the costly groups (behind the
+                    // glass) taken last left a tail: at 90 % of the C3 launch only 25 of 2,048
+                    // waves were still running (WAVEPROF timeline).  C3 frame 445 -> 407 ms
+                    // (probe included; order 1: 408, top 20 / 35 %: 408 / 408 ms)
+                    const int order = std::getenv("NART_RQ_ORDER") ? std::atoi(std::getenv("NART_RQ_ORDER")) : 2;
+                    if (order == 1 || order == 2) {
+                        RenderArgs pb = b;  // cost probe: the first sample of every pixel
+                        pb.spp = 1;
+                        pb.cost = ctx->d_cost;
+                        pb.ghead = nullptr;
+                        hipLaunchKernelGGL((k_render<MAXL, true, ENV, false>), dim3(blocks), block, lds, st, ctx->scene, pb);
+                        const uint32_t ng = (n + 63) / 64;
+                        const dim3 gg((ng + 255) / 256);
+                        hipLaunchKernelGGL(k_group_keys, gg, block, 0, st, ctx->d_cost, n, ctx->d_keys[0], ctx->d_vals[0]);
+                        size_t tmp = ctx->cap_sort_tmp;
+                        HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->d_sort_tmp, tmp, ctx->d_keys[0], ctx->d_keys[1],
+                                                                  ctx->d_vals[0], ctx->d_vals[1], (int)ng, 0, 32, st));
+                        if (order == 1) {
+                            b.gorder = ctx->d_vals[1];
+                        } else {
+                            const double f = std::getenv("NART_RQ_TOPF") ? std::atof(std::getenv("NART_RQ_TOPF")) : 10.0;
+                            const uint32_t E = (uint32_t)std::min<double>(ng, std::max(0.0, f) * 0.01 * ng);
+                            hipLaunchKernelGGL(k_group_class, gg, block, 0, st, ctx->d_vals[1], ng, E, ctx->d_keys[0],
+                                               ctx->d_vals[0]);
+                            tmp = ctx->cap_sort_tmp;
+                            HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->d_sort_tmp, tmp, ctx->d_keys[0], ctx->d_keys[1],
+                                                                      ctx->d_vals[0], ctx->d_queue, (int)ng, 0, 1, st));
+                            b.gorder = ctx->d_queue;
+                        }
+                    }
                     // launches are counted in blocks of 256 threads
                     blocks = std::min(blocks, (uint32_t)std::max(1, cus * std::max(per_cu_rq, 1)) * (NART_RQ_BLOCK / 256));
                 }

@@ -120,6 +120,26 @@ def test_queue_speculative_pairs(gpu, glass_scene, monkeypatch, pairs):
     assert _bits_equal(g, r), _report(g, r)
 
 
+@pytest.fixture(scope="module")
+def full_frame_1spp(glass_scene):
+    """The C3 frame size at 1 spp: ~16 rounds of resident waves, so the ray-queue kernel runs its
+    wave-group refill (render.hip launch_render, R >= 12)."""
+    p = _params(glass_scene, 1920, 1080, 1)
+    return p, oracle.Oracle(glass_scene).render(p)
+
+
+@pytest.mark.parametrize("order", ["0", "1", "2"], ids=["slot-order", "costliest-first", "top-class-first"])
+def test_group_refill_order(gpu, glass_scene, full_frame_1spp, monkeypatch, order):
+    """Wave-group refill on a full frame with the groups taken in slot order, costliest first
+    (cost probe + sort), or the costliest NART_RQ_TOPF % first: only the order of work
+    changes, so the frame must equal the oracle's bit for bit."""
+    monkeypatch.setenv("NART_RQ_ORDER", order)
+    monkeypatch.setenv("NART_RQ_TOPF", "15")
+    p, r = full_frame_1spp
+    g = nart_amd.HipRenderer(glass_scene, variant=0).render(p)
+    assert _bits_equal(g, r), _report(g, r)
+
+
 def test_queue_scheduler_environment(gpu, env_scene):
     p = _params(env_scene, 480, 300, 2)
     g = nart_amd.HipRenderer(env_scene, variant=0).render(p)
