@@ -564,7 +564,13 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             // costly pixels per first-round wave: few when the shard is small (their serial chains
             // bound the frame), all 64 (packed, launched first) when there are many rounds
             uint32_t k = R >= 3.0 ? 32u : 8u;  // measured on C3 shards of 1/2, 1/4, 1/8 of the frame
-            if (R >= 12.0 && mode == 2 && !std::getenv("NART_QUEUE_K")) {
+            // ray-queue kernel: wave-group refill from 6 rounds of resident waves (C3 1/2 shard, 8
+            // rounds: 241 -> 235 ms; C4 batches, ~9 rounds: 1385 -> 1566 Msamples/s).  Below that a
+            // wave of costly groups outlasts the rest (1/4 shard, 4 rounds: 146 -> 211 ms), and
+            // the probe-ordered pixel queue with priority lanes stays
+            static const double g_rounds =
+                std::getenv("NART_RQ_GROUP_MIN_ROUNDS") ? std::atof(std::getenv("NART_RQ_GROUP_MIN_ROUNDS")) : 6.0;
+            if (R >= (rq ? g_rounds : 12.0) && mode == 2 && !std::getenv("NART_QUEUE_K")) {
                 // many rounds: the slot order (costly waves interleaved with cheap ones in time)
                 // measured faster than any reordering; no probe.  The ray-queue kernel runs it on
                 // a persistent grid whose waves take wave-sized slot groups in that order
