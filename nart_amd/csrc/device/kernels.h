@@ -865,7 +865,7 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
         bm = 0;
         jst = rng;
         jfl = J_VER;
-        if (lane & 1) {
+        if (lane & (A.rq_pairs - 1u)) {
             s = A.spp;
             jfl = 0;
         }
@@ -990,78 +990,119 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                 }
             }
         }
-        // speculative pairs: commit verified results in sample order, check speculative starts,
-        // hand out the next jobs.  Both lanes of a pair evaluate the same function of the pair's
-        // two job records (exchanged with lane ^ 1) and keep their own half.
+        // speculative lane groups (A.rq_pairs = Q lanes per costly pixel, 2 or 4): commit verified
+        // results in sample order, check speculative starts, hand out the next jobs.  Every lane of
+        // a group evaluates the same function of the group's Q job records (exchanged with
+        // shuffles inside the group) and keeps its own record.  Jobs in flight always cover a
+        // contiguous run of samples [pF, hs]; a job becomes verified when it reaches the frontier
+        // with the frontier's true start state, otherwise every job of the run is dropped.
         if (A.rq_pairs) {
-            const uint32_t o_s = __shfl_xor(s, 1), o_st = __shfl_xor(jst, 1), o_fl = __shfl_xor(jfl, 1);
-            const uint32_t o_end = __shfl_xor(jend, 1), o_nd = __shfl_xor(nd, 1);
-            const uint32_t o_w = __shfl_xor(waiting ? 1u : 0u, 1);
-            if (pm) {
-                const uint32_t NONE = A.spp;
-                // my job record and my partner's (scalars: no dynamically indexed arrays)
-                uint32_t ms = s, mst = jst, mfl = jfl, os = o_s, ost = o_st, ofl = o_fl;
-                bool mchg = false, ochg = false;  // job dropped or handed out in this step
+            const uint32_t Q = A.rq_pairs, gb = (uint32_t)lane & ~(Q - 1u), mi = (uint32_t)lane & (Q - 1u);
+            const uint32_t NONE = A.spp;
+            uint32_t gs[4], gst[4], gfl[4], gend[4], gnd[4];
+            bool gw[4], gchg[4];
 #pragma unroll
-                for (int it = 0; it < 2; ++it) {
-                    const bool cm = ms == pF && (mfl & J_VER) && (mfl & J_FIN);
-                    const bool co = os == pF && (ofl & J_VER) && (ofl & J_FIN);
-                    if (!cm && !co) break;
-                    if (cm) A.Lout[soff + (uint64_t)pF * sstr] = jres;
+            for (uint32_t k = 0; k < 4; ++k) {
+                const int src = (int)(gb + (k < Q ? k : 0u));
+                gs[k] = __shfl(s, src);
+                gst[k] = __shfl(jst, src);
+                gfl[k] = __shfl(jfl, src);
+                gend[k] = __shfl(jend, src);
+                gnd[k] = __shfl(nd, src);
+                gw[k] = __shfl(waiting ? 1u : 0u, src) != 0u;
+                gchg[k] = false;
+                if (k >= Q) {
+                    gs[k] = NONE;
+                    gfl[k] = 0u;
+                }
+            }
+            if (pm) {
+#pragma unroll
+                for (uint32_t it = 0; it < 4; ++it) {
+                    uint32_t kc = 4u;
+#pragma unroll
+                    for (uint32_t k = 0; k < 4; ++k)
+                        if (gs[k] == pF && (gfl[k] & J_VER) && (gfl[k] & J_FIN)) kc = k;
+                    if (kc == 4u) break;
+                    if (kc == mi) A.Lout[soff + (uint64_t)pF * sstr] = jres;
                     // majority vote over the committed samples' draw counts
-                    const uint32_t n = cm ? nd : o_nd, bv = bm & 0xFFFFu, bc = bm >> 16;
+                    uint32_t n = 0u, e = 0u;
+#pragma unroll
+                    for (uint32_t k = 0; k < 4; ++k)
+                        if (k == kc) {
+                            n = gnd[k];
+                            e = gend[k];
+                        }
+                    const uint32_t bv = bm & 0xFFFFu, bc = bm >> 16;
                     bm = (n == bv) ? (bv | ((bc + 1u) << 16)) : (bc == 0u ? (n | (1u << 16)) : (bv | ((bc - 1u) << 16)));
-                    pR = cm ? jend : o_end;
+                    pR = e;
                     ++pF;
-                    // the other job is the new frontier's: keep it iff it started from the true state
-                    if (cm) {
-                        ms = NONE;
-                        mfl = 0;
-                        if (os == pF && !(ofl & J_VER)) {
-                            if (ost == pR) {
-                                ofl |= J_VER;
-                            } else {
-                                ofl = o_w ? J_DOOM : 0u;
-                                os = NONE;
-                                ochg = true;
-                            }
+#pragma unroll
+                    for (uint32_t k = 0; k < 4; ++k)
+                        if (k == kc) {
+                            gs[k] = NONE;
+                            gfl[k] = 0u;
                         }
-                    } else {
-                        os = NONE;
-                        ofl = 0;
-                        if (ms == pF && !(mfl & J_VER)) {
-                            if (mst == pR) {
-                                mfl |= J_VER;
-                            } else {
-                                mfl = waiting ? J_DOOM : 0u;
-                                ms = NONE;
-                                mchg = true;
-                            }
+                    // the new frontier's job: keep it iff it started from the true state, else
+                    // drop every job of the run (their starts were predicted from it)
+                    bool bad = false;
+#pragma unroll
+                    for (uint32_t k = 0; k < 4; ++k)
+                        if (gs[k] == pF && !(gfl[k] & J_VER)) {
+                            if (gst[k] == pR) gfl[k] |= J_VER;
+                            else bad = true;
                         }
+                    if (bad) {
+#pragma unroll
+                        for (uint32_t k = 0; k < 4; ++k)
+                            if (gs[k] != NONE) {
+                                gfl[k] = gw[k] ? J_DOOM : 0u;
+                                gs[k] = NONE;
+                                gchg[k] = true;
+                            }
                     }
                 }
-                // next jobs (the even lane first): the frontier from its true state, else the
-                // sample after it from the predicted state (once a draw count has been seen)
-                auto hand_out = [&](uint32_t& xs, uint32_t& xst, uint32_t& xfl, bool& xchg, uint32_t ys) {
-                    if (xs != NONE || (xfl & J_DOOM)) return;
-                    if (pF < A.spp && ys != pF) {
-                        xs = pF;
-                        xst = pR;
-                        xfl = J_VER;
-                        xchg = true;
-                    } else if (pF + 1u < A.spp && ys == pF && (bm >> 16) != 0u) {
-                        xs = pF + 1u;
-                        xst = rng_jump(pR, bm & 0xFFFFu);
-                        xfl = 0;
-                        xchg = true;
+                // next jobs, in lane order: the frontier from its true state when no job holds it,
+                // else the sample after the run from the last job's end state (if finished) or
+                // its start advanced by the predicted number of draws
+#pragma unroll
+                for (uint32_t k = 0; k < 4; ++k) {
+                    if (gs[k] != NONE || (gfl[k] & J_DOOM) || k >= Q) continue;
+                    uint32_t hs = NONE, hst = 0u, hfl = 0u, hend = 0u;
+#pragma unroll
+                    for (uint32_t j = 0; j < 4; ++j)
+                        if (gs[j] != NONE && (hs == NONE || gs[j] > hs)) {
+                            hs = gs[j];
+                            hst = gst[j];
+                            hfl = gfl[j];
+                            hend = gend[j];
+                        }
+                    if (hs == NONE) {
+                        if (pF < A.spp) {
+                            gs[k] = pF;
+                            gst[k] = pR;
+                            gfl[k] = J_VER;
+                            gchg[k] = true;
+                        }
+                    } else if (hs + 1u < A.spp && (bm >> 16) != 0u) {
+                        gs[k] = hs + 1u;
+                        gst[k] = (hfl & J_FIN) ? hend : rng_jump(hst, bm & 0xFFFFu);
+                        gfl[k] = 0u;
+                        gchg[k] = true;
                     }
-                };
-                if ((lane & 1) == 0) {
-                    hand_out(ms, mst, mfl, mchg, os);
-                    hand_out(os, ost, ofl, ochg, ms);
-                } else {
-                    hand_out(os, ost, ofl, ochg, ms);
-                    hand_out(ms, mst, mfl, mchg, os);
+                }
+                uint32_t ms = NONE, mst = 0u, mfl = 0u;
+                bool mchg = false, any_doom = false, all_none = true;
+#pragma unroll
+                for (uint32_t k = 0; k < 4; ++k) {
+                    if (k == mi) {
+                        ms = gs[k];
+                        mst = gst[k];
+                        mfl = gfl[k];
+                        mchg = gchg[k];
+                    }
+                    any_doom = any_doom || (gfl[k] & J_DOOM);
+                    all_none = all_none && gs[k] == NONE;
                 }
                 if (mchg) {
                     need_shade = false;  // a dropped job's pending hit, or a job that starts afresh
@@ -1070,7 +1111,7 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                 s = ms;
                 jst = mst;
                 jfl = mfl;
-                if (pF >= A.spp && ms == NONE && os == NONE && !((mfl | ofl) & J_DOOM)) pm = false;
+                if (pF >= A.spp && all_none && !any_doom) pm = false;
             }
         }
         RQ_MARK(0);

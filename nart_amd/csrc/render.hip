@@ -426,13 +426,14 @@ __global__ void k_flag_top(const uint32_t* sorted, uint32_t n, uint32_t E, uint3
 // Queue: in the first round of W waves, lanes j < k of wave w take the costly pixel of rank
 // j*W + w (each wave holds k of them); every other position takes the remaining pixels in
 // slot order (spatially coherent waves).
-// With prio set (k_render_rq) the costly entries carry RQ_PRIO_BIT; with pairs each costly pixel
-// goes to two adjacent lanes (2j, 2j + 1) with RQ_PAIR_BIT too, and the queue is n + k*W long.
+// With prio set (k_render_rq) the costly entries carry RQ_PRIO_BIT; with pairs = Q (2 or 4) each
+// costly pixel goes to Q adjacent lanes (Qj .. Qj + Q - 1) with RQ_PAIR_BIT too, and the queue is
+// n + (Q - 1)*k*W long.
 __global__ void k_build_queue(const uint32_t* top, const uint32_t* rest, uint32_t n, uint32_t W, uint32_t k,
                               uint32_t prio, uint32_t pairs, uint32_t* queue) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t per = pairs ? 2u : 1u, kk = per * k;  // first-round lanes of the costly pixels
-    if (p >= n + (pairs ? k * W : 0u)) return;
+    const uint32_t per = pairs ? pairs : 1u, kk = per * k;  // first-round lanes of the costly pixels
+    if (p >= n + (per - 1u) * k * W) return;
     const uint32_t g = 64u * W;
     if (p < g) {
         const uint32_t w = p / 64u, j = p % 64u;
@@ -466,6 +467,9 @@ __global__ void k_iota(uint32_t* v, uint32_t n) {
     if (i < n) v[i] = i;
 }
 
+#ifndef NART_RQ_GROUP_LANES
+#define NART_RQ_GROUP_LANES 2
+#endif
 int queue_mode() {
     static int m = -1;
     if (m < 0) {
@@ -654,14 +658,16 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                 // (1/2 C3 shard 238 -> 249 ms, C4 batches 3175 -> 3381 ms with them on)
                 const int prio_env = std::getenv("NART_RQ_PRIO") ? std::atoi(std::getenv("NART_RQ_PRIO")) : 1;
                 const bool prio_on = prio_env == 2 || (prio_env == 1 && R < q_rounds);
-                const bool pairs_on = !std::getenv("NART_RQ_PAIRS") || std::atoi(std::getenv("NART_RQ_PAIRS")) != 0;
+                // NART_RQ_PAIRS: lanes per costly pixel (0 off; 1 or 2 pairs; 4 groups of four)
+                const int pe = std::getenv("NART_RQ_PAIRS") ? std::atoi(std::getenv("NART_RQ_PAIRS")) : NART_RQ_GROUP_LANES;
+                const uint32_t Q = pe <= 0 ? 0u : (pe >= 4 ? 4u : 2u);
                 const uint32_t pbit = (rq && prio_on) ? RQ_PRIO_BIT : 0u;
-                const bool pairs = pbit && pairs_on && 2u * k <= 64u;
-                const uint32_t qlen = n + (pairs ? k * W : 0u);
+                const uint32_t pairs = (pbit && Q && Q * k <= 64u) ? Q : 0u;
+                const uint32_t qlen = n + (pairs ? (pairs - 1u) * k * W : 0u);
                 hipLaunchKernelGGL(k_build_queue, dim3((qlen + 255) / 256), block, 0, st, ctx->d_vals[1], ctx->d_vals[0],
-                                   n, W, k, pbit, pairs ? 1u : 0u, ctx->d_queue);
+                                   n, W, k, pbit, pairs, ctx->d_queue);
                 b.rq_prio = pbit ? 1u : 0u;
-                b.rq_pairs = pairs ? 1u : 0u;
+                b.rq_pairs = pairs;
                 b.qlen = qlen;
             }
             b.queue = ctx->d_queue;
@@ -1512,16 +1518,17 @@ int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t
         p->integrator == NART_INTEGRATOR_PATH && n <= 65536) {
         // development probe of the speculative pairs: every pixel of the rect on two lanes
         // (the ray-queue kernel alone, camera rays included; no work queue refill)
-        rc = ensure_queue(ctx, 2 * n);
+        const uint32_t Q = std::atoi(std::getenv("NART_SAMPLES_PAIRS")) >= 4 ? 4u : 2u;  // lanes per pixel
+        rc = ensure_queue(ctx, Q * n);
         if (rc) return rc;
-        std::vector<uint32_t> q(2 * n);
-        for (uint32_t i = 0; i < n; ++i) q[2 * i] = q[2 * i + 1] = i | RQ_PRIO_BIT | RQ_PAIR_BIT;
+        std::vector<uint32_t> q(Q * n);
+        for (uint32_t i = 0; i < Q * n; ++i) q[i] = (i / Q) | RQ_PRIO_BIT | RQ_PAIR_BIT;
         HIPCHK(hipMemcpy(ctx->d_queue, q.data(), q.size() * 4, hipMemcpyHostToDevice));
         RenderArgs r2 = ra;
         r2.queue = ctx->d_queue;
-        r2.qlen = 2 * n;
+        r2.qlen = Q * n;
         r2.rq_prio = 1;
-        r2.rq_pairs = 1;
+        r2.rq_pairs = Q;
         r2.rq_quorum = 0;
         r2.lds_nodes = render_lds_nodes(ctx, rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK), NART_RQ_BLOCK / 256);
         const size_t lds_rq = rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK) + (size_t)r2.lds_nodes * sizeof(BVHNode);
@@ -1532,7 +1539,7 @@ int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t
             attr = true;
         }
         if (ctx->has_env || p->bounces > 10) return fail(ctx, NART_E_UNSUPPORTED, "pairs probe: glass-like scenes only");
-        hipLaunchKernelGGL(kern, dim3((2 * n + NART_RQ_BLOCK - 1) / NART_RQ_BLOCK), dim3(NART_RQ_BLOCK), lds_rq, 0,
+        hipLaunchKernelGGL(kern, dim3((Q * n + NART_RQ_BLOCK - 1) / NART_RQ_BLOCK), dim3(NART_RQ_BLOCK), lds_rq, 0,
                            ctx->scene, r2);
         HIPCHK(hipGetLastError());
     } else {

@@ -107,7 +107,7 @@ def test_queue_scheduler_frames(gpu, glass_scene, monkeypatch, w, h, spp, prio):
     assert _bits_equal(g, r), _report(g, r)
 
 
-@pytest.mark.parametrize("pairs", ["1", "0"], ids=["speculative-pairs", "single-lanes"])
+@pytest.mark.parametrize("pairs", ["2", "4", "0"], ids=["speculative-pairs", "speculative-quads", "single-lanes"])
 def test_queue_speculative_pairs(gpu, glass_scene, monkeypatch, pairs):
     """A shard of ~1.2 rounds of resident waves at 24 spp: the costliest pixels run as speculative
     lane pairs (one lane on the chain's frontier sample, the other on the next sample from a

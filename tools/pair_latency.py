@@ -1,6 +1,6 @@
 """Chain latency of costly glassSphere pixels with and without speculative lane pairs
-(development aid): nart_hip_render_samples of small rects, NART_SAMPLES_PAIRS=0/1, results
-compared bit for bit between the two."""
+(development aid): nart_hip_render_samples of small rects, NART_SAMPLES_PAIRS=0/2/4 (lanes per
+pixel), results compared bit for bit with the single-lane run."""
 import os
 import sys
 import time
@@ -24,7 +24,7 @@ def main():
     gpu.render_samples(p, 0, 0, 4, 4)
     for (x, y, w, h) in [(928, 712, 1, 1), (928, 712, 4, 1), (928, 712, 16, 1), (928, 712, 16, 4), (100, 100, 16, 4)]:
         res = {}
-        for pairs in ("0", "1"):
+        for pairs in ("0", "2", "4"):
             os.environ["NART_SAMPLES_PAIRS"] = pairs
             best = 1e9
             for _ in range(2):
@@ -32,9 +32,10 @@ def main():
                 out = gpu.render_samples(p, x, y, w, h)
                 best = min(best, time.perf_counter() - t)
             res[pairs] = (best, out)
-        same = np.array_equal(np.asarray(res["0"][1]).view(np.uint32), np.asarray(res["1"][1]).view(np.uint32))
-        print("rect (%d,%d) %dx%d  single %.2f ms  pairs %.2f ms  identical %s" % (
-            x, y, w, h, res["0"][0] * 1e3, res["1"][0] * 1e3, same), flush=True)
+        same = all(np.array_equal(np.asarray(res["0"][1]).view(np.uint32), np.asarray(res[q][1]).view(np.uint32))
+                   for q in ("2", "4"))
+        print("rect (%d,%d) %dx%d  single %.2f ms  pairs %.2f ms  quads %.2f ms  identical %s" % (
+            x, y, w, h, res["0"][0] * 1e3, res["2"][0] * 1e3, res["4"][0] * 1e3, same), flush=True)
 
 
 if __name__ == "__main__":
