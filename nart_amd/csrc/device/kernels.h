@@ -792,8 +792,12 @@ NHD size_t rq_lds_bytes(uint32_t stack_depth, uint32_t block) {
            (size_t)waves * 2 * RQ_RING;
 }
 
+// 512-thread blocks: one block of 8 waves per CU shares one copy of the staged BVH nodes (twice
+// as many nodes in LDS).  With the wave-group refill (no wave waits for its block) C3 392 vs
+// 407 ms per frame (profiles/r02m_rq_block_ab.log); before it, blocks retiring as a whole made
+// 256 faster (132.6 vs 121.5 ms at 64 spp)
 #ifndef NART_RQ_BLOCK
-#define NART_RQ_BLOCK 256
+#define NART_RQ_BLOCK 512
 #endif
 template <int MAXL, bool COUNT, bool ENV>
 __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(DScene S, RenderArgs A) {

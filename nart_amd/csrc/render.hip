@@ -674,8 +674,10 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             if (refill) {
                 HIPCHK(hipMemsetAsync(ctx->d_qhead, 0, sizeof(uint32_t), st));
                 b.qhead = ctx->d_qhead;
-                b.qbase = resident * 256;
-                blocks = resident;
+                // whole ray-queue blocks, so that every first-round lane's entry lies below qbase
+                const uint32_t per = rq ? NART_RQ_BLOCK / 256 : 1u;
+                blocks = (resident + per - 1u) / per * per;
+                b.qbase = blocks * 256;
             }
         }
     }
