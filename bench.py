@@ -3,6 +3,11 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
+Without a launcher, --gpus N > 1 spawns the N rank processes itself (nart_amd.dist.spawn_ranks,
+before any GPU call); under a launcher, --gpus must equal WORLD_SIZE or the bench exits non-zero.
+NART_DIST_BACKEND=gloo (host-staged tiles) and NART_BENCH_SAME_DEVICE=1 (every rank on GPU 0)
+rehearse the multi-rank path on a one-GPU box; the default is RCCL ("nccl"), one GPU per rank.
+
 A step renders the whole frame once: every rank renders an interleaved share of the
 reference's 16x16 buckets (all spp of their pixels) into device tiles, the tiles are gathered
 to rank 0 over RCCL, and rank 0 combines them in bucket raster order (render.cpp:183-203),
@@ -32,7 +37,7 @@ import torch  # noqa: E402
 
 import nart_amd  # noqa: E402
 from nart_amd import scenes  # noqa: E402
-from nart_amd.dist import BucketShard  # noqa: E402
+from nart_amd.dist import BucketShard, spawn_ranks  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -125,18 +130,39 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    # smaller frames of the same scene (multi-rank rehearsals and tests; not a bench line)
+    ap.add_argument("--size", default=None, help="WxHxSPP override, e.g. 320x180x8")
+    ap.add_argument("--dump-image", default=None, help="rank 0 saves the combined float32 image (.npy)")
     a = ap.parse_args()
     cfg = CONFIGS[a.config]
     W, H, SPP = cfg["w"], cfg["h"], cfg["spp"]
+    if a.size:
+        W, H, SPP = (int(v) for v in a.size.lower().split("x"))
 
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        # no launcher: start the N ranks here, before this process touches a GPU
+        sys.exit(spawn_ranks(a.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        print("bench.py: --gpus %d but the job has %d rank(s) (WORLD_SIZE); refusing to report a %d-GPU number"
+              % (a.gpus, world, a.gpus), file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    backend = os.environ.get("NART_DIST_BACKEND", "nccl")
+    if os.environ.get("NART_BENCH_SAME_DEVICE", "0") not in ("", "0"):
+        local = 0  # rehearsal: every rank on GPU 0 (RCCL needs distinct GPUs, so use gloo)
     torch.cuda.set_device(local)
     if dist:
         import torch.distributed as td
-        td.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            td.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            td.init_process_group(backend)
+        world = td.get_world_size()
+        print("bench.py: rank %d of %d on %s (%s), backend %s" % (rank, world, torch.cuda.get_device_name(local),
+                                                                  "cuda:%d" % local, backend), file=sys.stderr)
 
     scene_dir = os.path.join("/tmp", "nart_bench_scene_%s_%d" % (a.config, os.getpid()))
     path = cfg["scene"](scene_dir)
@@ -190,7 +216,7 @@ def main():
     dt = time.perf_counter() - t0
     if dist:
         import torch.distributed as td
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         td.all_reduce(tt, op=td.ReduceOp.MAX)
         dt = float(tt.item())
 
@@ -236,8 +262,11 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": cfg["data"],
-            "config": {"workload": cfg["workload"], "image": [W, H], "spp": SPP, "buckets": nb,
-                       "parallelism": "buckets interleaved over %d rank(s), RCCL gather to rank 0" % world},
+            "config": {"workload": cfg["workload"] if not a.size else "%s, resized to %dx%d %dspp (rehearsal, not "
+                                                                              "the bench workload)" % (
+                           cfg["workload"], W, H, SPP), "image": [W, H], "spp": SPP, "buckets": nb,
+                       "parallelism": "buckets interleaved over %d rank(s), %s gather to rank 0" % (
+                           world, {"nccl": "RCCL"}.get(backend, backend))},
             "roofline": roofline,
             "kernel_ms_per_step": round(st.kernel_ms / a.steps, 3),
             "splat_ms_per_step": round(st.splat_ms / a.steps, 3),
@@ -256,6 +285,8 @@ def main():
             out["parity"] = {"buckets_compared": int(len(ids)), "tile_floats": int(gt.size),
                              "bit_identical": bool(np.array_equal(gt.view(np.uint32), ref_tiles.view(np.uint32))),
                              "max_abs_diff": float(diff.max()), "rmse": float(np.sqrt((diff ** 2).mean()))}
+        if a.dump_image:
+            np.save(a.dump_image, image.cpu().numpy())
         print(json.dumps(out), flush=True)
     if dist:
         import torch.distributed as td

@@ -10,8 +10,9 @@
  * (src/materials/<type>material.cpp) and lights (src/lights/<type>light.cpp) run on the device.
  *
  * All entry points return NART_OK (0) or a negative NART_E_* code (nart_scene.h); no C++
- * exception crosses the ABI and nothing aborts.  A context owns all device memory for one
- * device and is not thread-safe (one caller thread, like the reference's main thread).
+ * exception crosses the ABI and nothing aborts.  A context owns all device memory of its
+ * device(s) (and, multi-device, its streams and RCCL communicator) and is not thread-safe (one
+ * caller thread, like the reference's main thread).
  */
 #ifndef NART_HIP_H
 #define NART_HIP_H
@@ -50,6 +51,28 @@ typedef struct nart_render_stats {
 int nart_hip_create(const nart_scene_blob* scene, int device_id, nart_ctx** out);
 void nart_hip_destroy(nart_ctx* ctx);
 const char* nart_hip_last_error(const nart_ctx* ctx);
+
+/* Multi-GPU context over device_ids[0..n_devices) of this node, replacing the reference's
+   tbb::task_group over host cores (render.cpp:152-177): the scene is uploaded to every device;
+   nart_hip_render shards the buckets (bucket b -> device b % n, nart_hip_shard_buckets), renders
+   the shares concurrently (one host thread per device), gathers the tiles to device_ids[0] with
+   the library's own RCCL communicator (ncclCommInitAll over the list; ncclSend/ncclRecv over
+   xGMI) and combines them there in bucket raster order (render.cpp:183-203), so the image is
+   bit-identical for any n.  n_devices == 1 is exactly nart_hip_create.  Repeated ordinals (a
+   rehearsal of n devices on fewer GPUs) gather with device copies, since RCCL needs distinct
+   GPUs; NART_GATHER=rccl|copy overrides.  NART_E_RCCL if the communicator cannot be built. */
+int nart_hip_create_multi(const nart_scene_blob* scene, const int* device_ids, int n_devices, nart_ctx** out);
+
+/* Devices of a context (1 for nart_hip_create) and whether its gather runs over RCCL. */
+int nart_hip_context_devices(const nart_ctx* ctx, int* n_devices, int* uses_rccl);
+
+/* HIP devices visible to this process. */
+int nart_hip_device_count(int* count);
+
+/* Host only: the buckets device device_index of n_devices renders (ascending ids b with
+   b % n_devices == device_index) into ids (may be null to query the count). */
+int nart_hip_shard_buckets(uint32_t n_buckets, uint32_t n_devices, uint32_t device_index, uint32_t* ids,
+                           uint32_t* count);
 
 /* Whole-session render, Render()-equivalent: fills a caller-owned host buffer of
    totalW*totalH nart_pixel (render.cpp:114-206 contract, render.h:18-21 layout). */

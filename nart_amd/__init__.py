@@ -5,7 +5,8 @@ bindings; see DESIGN.md for the architecture and INTEGRATION.md for the drop-in 
 """
 from .api import (HIP_SYMBOLS, PIXEL_FLOATS, SCENE_SYMBOLS, HipRenderer, bvh_info, NartError, NativeLibraryMissing,  # noqa: F401
                   RenderParams, RenderStats, Scene, combine_tiles, default_params, filter_table, finalize,
-                  hip_lib, load_sessions, parse_args, read_exr, scene_lib, session_geometry, write_exr)
+                  hip_lib, load_sessions, parse_args, read_exr, scene_lib, session_geometry, shard_buckets,
+                  write_exr)
 
 __all__ = ["HipRenderer", "bvh_info", "NartError", "NativeLibraryMissing", "RenderParams", "RenderStats", "Scene",
            "combine_tiles", "default_params", "filter_table", "finalize", "load_sessions", "parse_args", "read_exr",

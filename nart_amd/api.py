@@ -71,6 +71,21 @@ class RenderStats(ctypes.Structure):
 
 
 _P = ctypes.c_void_p
+
+
+class _Texture(ctypes.Structure):
+    """nart_texture (include/nart_scene.h)."""
+    _fields_ = [("width", ctypes.c_uint32), ("height", ctypes.c_uint32), ("rgba", _P)]
+
+
+class _BlobHead(ctypes.Structure):
+    """Leading fields of nart_scene_blob (include/nart_scene.h)."""
+    _fields_ = [("num_triangles", ctypes.c_uint32), ("num_meshes", ctypes.c_uint32),
+                ("num_materials", ctypes.c_uint32), ("num_lights", ctypes.c_uint32),
+                ("num_textures", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("triangles", _P),
+                ("meshes", _P), ("materials", _P), ("lights", _P), ("textures", ctypes.POINTER(_Texture))]
+
+
 _SCENE_SIGS = {
     "nart_scene_load": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(_P)]),
     "nart_scene_blob_of": (_P, [_P]),
@@ -106,6 +121,11 @@ _HIP_SIGS = {
     "nart_hip_set_splat_mode": (ctypes.c_int, [_P, ctypes.c_int]),
     "nart_hip_splat_thresholds": (ctypes.c_int, [ctypes.c_float, _P]),
     "nart_hip_bvh_info": (ctypes.c_int, [_P, ctypes.POINTER(BvhInfo)]),
+    "nart_hip_create_multi": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(_P)]),
+    "nart_hip_context_devices": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "nart_hip_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "nart_hip_shard_buckets": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                              ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
 }
 SCENE_SYMBOLS = tuple(_SCENE_SIGS)
 HIP_SYMBOLS = tuple(_HIP_SIGS)
@@ -241,6 +261,27 @@ class Scene:
         c = ctypes.cast(self.blob, ctypes.POINTER(ctypes.c_uint32))
         return {"triangles": c[0], "meshes": c[1], "materials": c[2], "lights": c[3], "textures": c[4]}
 
+    def _view(self):
+        return ctypes.cast(self.blob, ctypes.POINTER(_BlobHead)).contents
+
+    def triangles(self):
+        """(n, 24) float32 copy of the blob's triangles (nart_triangle: v0 v1 v2 n0 n1 n2 uv0 uv1 uv2)."""
+        h = self._view()
+        if not h.num_triangles:
+            return np.zeros((0, 24), np.float32)
+        return np.ctypeslib.as_array(ctypes.cast(h.triangles, ctypes.POINTER(ctypes.c_float)),
+                                     shape=(h.num_triangles * 24,)).copy().reshape(-1, 24)
+
+    def textures(self):
+        """Loaded textures as (H, W, 4) uint16 half bit patterns (top row first), in load order."""
+        h = self._view()
+        out = []
+        for i in range(h.num_textures):
+            t = h.textures[i]
+            out.append(np.ctypeslib.as_array(ctypes.cast(t.rgba, ctypes.POINTER(ctypes.c_uint16)),
+                                             shape=(t.height * t.width * 4,)).copy().reshape(t.height, t.width, 4))
+        return out
+
     def close(self):
         if self._h:
             self._lib.nart_scene_free(self._h)
@@ -253,17 +294,35 @@ class Scene:
             pass
 
 
-class HipRenderer:
-    """nart_ctx: the scene resident on one GPU; Render()-equivalent entry points."""
+def shard_buckets(n_buckets, n_devices, device_index):
+    """Host only: the bucket ids a multi-device context renders on device_index (b % n == index)."""
+    lib = hip_lib()
+    cnt = ctypes.c_uint32()
+    rc = lib.nart_hip_shard_buckets(n_buckets, n_devices, device_index, None, ctypes.byref(cnt))
+    if rc != NART_OK:
+        raise NartError(rc, "nart_hip_shard_buckets")
+    ids = np.zeros(max(1, cnt.value), np.uint32)
+    lib.nart_hip_shard_buckets(n_buckets, n_devices, device_index,
+                               ids.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(cnt))
+    return ids[:cnt.value]
 
-    def __init__(self, scene, device=0, variant=None, splat_mode=None):
+
+class HipRenderer:
+    """nart_ctx: the scene resident on one GPU (device) or on several (devices=[...], one
+    process, library-owned RCCL gather: nart_hip_create_multi); Render()-equivalent entry points."""
+
+    def __init__(self, scene, device=0, variant=None, splat_mode=None, devices=None):
         self._lib = hip_lib()
         self.scene = scene
-        self.device = device
+        self.device = device if devices is None else devices[0]
         self._ctx = _P()
-        rc = self._lib.nart_hip_create(scene.blob, device, ctypes.byref(self._ctx))
+        if devices is None:
+            rc = self._lib.nart_hip_create(scene.blob, device, ctypes.byref(self._ctx))
+        else:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            rc = self._lib.nart_hip_create_multi(scene.blob, arr, len(devices), ctypes.byref(self._ctx))
         if rc != NART_OK:
-            raise NartError(rc, "nart_hip_create failed on device %d" % device)
+            raise NartError(rc, "nart_hip_create failed on device(s) %s" % (devices if devices is not None else device))
         if variant is not None:
             self.set_variant(variant)
         if splat_mode is not None:
@@ -282,6 +341,12 @@ class HipRenderer:
     def _check(self, rc):
         if rc != NART_OK:
             raise NartError(rc, self._lib.nart_hip_last_error(self._ctx).decode())
+
+    def devices(self):
+        """(number of devices, gather over RCCL) of this context."""
+        n, r = ctypes.c_int(), ctypes.c_int()
+        self._check(self._lib.nart_hip_context_devices(self._ctx, ctypes.byref(n), ctypes.byref(r)))
+        return n.value, bool(r.value)
 
     def set_counters(self, on):
         self._check(self._lib.nart_hip_set_counters(self._ctx, 1 if on else 0))

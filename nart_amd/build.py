@@ -51,7 +51,7 @@ def hip_source_sha():
     profiles/pmc_latest.json's HBM traffic) to the kernel code it was measured on."""
     import hashlib
     h = hashlib.sha256()
-    for f in _sources("render.hip", "device", "host/bvh_build.cpp", "host/bvh_build.h"):
+    for f in _sources("render.hip", "device", "host/bvh_build.cpp", "host/bvh_build.h", "host/multi_gpu.h"):
         h.update(os.path.relpath(f, CSRC).encode())
         with open(f, "rb") as fh:
             h.update(fh.read())

@@ -133,11 +133,11 @@ struct DScene {
     const uint32_t* oc_chunks;  // (tri_first, tri_count) into oc_tris
     const uint32_t* oc_tris;    // global triangle ids, chunk insertion order
     const int32_t* tri_leaf;    // leaf node of each triangle, -1 if unreachable
-    uint32_t* oc_lock;          // [oc_pool] replay heap ownership
-    unsigned long long* oc_heap;// [oc_pool][oc_cap] (key bits | node << 32)
+    uint32_t* oc_lock;          // [oc_pool] replay heap ownership (a wave's 64 heaps per entry)
+    unsigned long long* oc_heap;// [oc_pool][64][oc_cap] (key bits | node << 32)
     int32_t oc_root;
     uint32_t oc_cap, oc_pool;
-    int32_t oc_exact;           // 0 disables the emulation (A/B only; not reference behaviour)
+    int32_t oc_exact;           // 0 disables the emulation (A/B only; not reference behaviour), 2 replays every query
     float oc_scale;             // max |coordinate| of the scene and camera (margins)
 };
 

@@ -186,16 +186,28 @@ ND bool oc_chunk(const DScene& S, const Ray& r, uint32_t first, uint32_t count, 
 }
 
 ND void oc_replay(const DScene& S, const Ray& r, float tmax, float& bestT, uint32_t& bestG) {
-    // own a heap slot
-    uint32_t slot = (uint32_t)((blockIdx.x * blockDim.x + threadIdx.x) * 2654435761u) % S.oc_pool;
-    for (;;) {
-        uint32_t expect = 0u;
-        if (__hip_atomic_compare_exchange_strong(S.oc_lock + slot, &expect, 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT))
-            break;
-        slot = slot + 1 == S.oc_pool ? 0 : slot + 1;
+    // The lanes of a wave that replay together share one pool entry of 64 heaps (one per lane),
+    // acquired by their lowest lane alone.  A lane never spins on a lock held by a wave-mate
+    // (wave-mates parked at the reconvergence point would never release it), and a holder waits
+    // for nothing until it releases, so every acquisition ends however small the pool.
+    const unsigned long long act = __ballot(1);
+    const int leader = __ffsll((unsigned long long)act) - 1;
+    const int lane = (int)__lane_id();
+    uint32_t ws = 0;
+    if (lane == leader) {
+        ws = (uint32_t)(((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 2654435761u) % S.oc_pool;
+        for (;;) {
+            uint32_t expect = 0u;
+            if (__hip_atomic_compare_exchange_strong(S.oc_lock + ws, &expect, 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT))
+                break;
+            ws = ws + 1 == S.oc_pool ? 0 : ws + 1;
+        }
     }
-    unsigned long long* h = S.oc_heap + (size_t)slot * S.oc_cap;
+    ws = (uint32_t)__shfl((int)ws, leader);
+    // a lane only reads heap entries it wrote during this replay (push before pop), so nothing a
+    // previous owner left behind is ever read
+    unsigned long long* h = S.oc_heap + ((size_t)ws * 64 + (size_t)lane) * S.oc_cap;
     float oa[3], da[3];
     oc_axes(r, oa, da);
     uint32_t n = 0;
@@ -226,7 +238,8 @@ ND void oc_replay(const DScene& S, const Ray& r, float tmax, float& bestT, uint3
         }
         if (n && isT < __uint_as_float((uint32_t)oc_ld(h))) break;
     }
-    __hip_atomic_store(S.oc_lock + slot, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    // every lane that entered has left the search loop (reconverged here)
+    if (lane == leader) __hip_atomic_store(S.oc_lock + ws, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     bestT = isT;
     bestG = isG;
 }
@@ -250,6 +263,7 @@ template <bool COUNT>
 ND void oc_resolve(const DScene& S, const Ray& r, float tmax, bool any, bool risky, uint32_t info, float t2,
                    float& bestT, uint32_t& bestG, TraceCounters& cnt) {
     if (!S.oc_exact) return;
+    if (S.oc_exact == 2) risky = true;  // NART_OCTREE_EXACT=2: every query replays the octree search (tests)
     int leaf = 0;
     const float bound = any ? tmax : t2;
     if (!risky) {

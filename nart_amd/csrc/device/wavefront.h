@@ -161,7 +161,6 @@ template <bool COUNT>
 __global__ __launch_bounds__(256) void k_wf_trace(DScene S, WFArgs A, uint32_t it) {
     extern __shared__ __attribute__((aligned(16))) int s_dyn[];
     int* sc = reinterpret_cast<int*>(reinterpret_cast<int2*>(s_dyn) + threadIdx.x);
-    float* stn = reinterpret_cast<float*>(s_dyn + A.R.stack_depth * blockDim.x) + threadIdx.x;
     const uint32_t cur = it & 1u, nxt = cur ^ 1u;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         A.counts[nxt] = 0;  // queues of the next iteration, filled by k_wf_shade(it)
@@ -205,7 +204,7 @@ __global__ __launch_bounds__(256) void k_wf_trace(DScene S, WFArgs A, uint32_t i
             }
         }
         if (__ballot(busy) == 0) break;
-        if (busy && trav_step<COUNT>(S, r, t, sc, stn, blockDim.x, cnt, nullptr, 0)) {
+        if (busy && trav_step<COUNT>(S, r, t, sc, nullptr, blockDim.x, cnt, nullptr, 0)) {
             busy = false;
             oc_resolve<COUNT>(S, r, t.tmax, t.any, t.risky, t.bestInfo, fminf(t.t2, oc_cull(S, t.bestT)), t.bestT, t.bestG, cnt);
             const bool hit = t.bestG != NO_HIT;

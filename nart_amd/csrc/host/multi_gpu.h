@@ -1,0 +1,210 @@
+// Multi-GPU render context (nart_hip_create_multi), included by render.hip.
+//
+// The reference renders a session's buckets with a tbb::task_group over every host core and sums
+// their tiles into the image in bucket raster order (render.cpp:152-203).  Here one process drives
+// N GPUs of the node:
+//   * the scene lives on every device (one single-device sub-context each, nart_hip_create);
+//   * bucket b belongs to device b % N (interleaved, so the costly regions of a frame spread over
+//     all devices; nart_hip_shard_buckets);
+//   * one host thread per device renders its share into device-resident tiles (render_buckets);
+//   * the tiles are gathered to device 0 with one RCCL group of ncclSend / ncclRecv over xGMI
+//     (library-owned communicator, ncclCommInitAll over the device list), permuted into bucket-id
+//     order and combined in bucket raster order on device 0 (k_combine) -- so the image is
+//     bit-identical for any N.
+// RCCL is loaded at run time (dlopen), so single-device use never needs it.  A device list with
+// repeated ordinals (a rehearsal of N ranks on fewer GPUs) gathers with device copies instead,
+// since an RCCL communicator needs distinct GPUs.  NART_GATHER=rccl|copy overrides the choice
+// (rccl on one device runs a self send/receive through RCCL).
+#pragma once
+
+#include <dlfcn.h>
+
+#include <mutex>
+#include <thread>
+
+namespace {
+
+struct RcclApi {
+    bool ok = false;
+    std::string err;
+    ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    const char* (*ErrStr)(ncclResult_t) = nullptr;
+};
+
+const RcclApi& rccl_api() {
+    static RcclApi api;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = nullptr;
+        for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+            if ((h = dlopen(name, RTLD_NOW | RTLD_LOCAL))) break;
+        if (!h) {
+            api.err = std::string("cannot load librccl: ") + dlerror();
+            return;
+        }
+        bool all = true;
+        auto sym = [&](auto& fn, const char* name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+            all = all && fn;
+        };
+        sym(api.CommInitAll, "ncclCommInitAll");
+        sym(api.CommDestroy, "ncclCommDestroy");
+        sym(api.GroupStart, "ncclGroupStart");
+        sym(api.GroupEnd, "ncclGroupEnd");
+        sym(api.Send, "ncclSend");
+        sym(api.Recv, "ncclRecv");
+        sym(api.ErrStr, "ncclGetErrorString");
+        api.ok = all;
+        if (!all) api.err = "librccl lacks ncclCommInitAll/ncclSend/ncclRecv";
+    });
+    return api;
+}
+
+#define RCCLCHK(call)                                                                              \
+    do {                                                                                           \
+        ncclResult_t r_ = (call);                                                                  \
+        if (r_ != ncclSuccess) return fail(ctx, NART_E_RCCL, std::string(#call ": ") + R.ErrStr(r_)); \
+    } while (0)
+
+// Bucket ids of device d out of n (bucket b -> device b % n), in ascending order.
+std::vector<uint32_t> shard_ids(uint32_t n_buckets, uint32_t n, uint32_t d) {
+    std::vector<uint32_t> ids;
+    for (uint32_t b = d; b < n_buckets; b += n) ids.push_back(b);
+    return ids;
+}
+
+// Gathered slabs (device d's tiles at slab_first(d), its i-th bucket being id d + i*n) -> tiles in
+// bucket-id order.  One block per bucket.
+__global__ void k_unshard(const float* slabs, float* by_id, uint32_t n_buckets, uint32_t n, uint32_t tile_floats) {
+    const uint32_t b = blockIdx.x;
+    if (b >= n_buckets) return;
+    const uint32_t d = b % n, i = b / n;
+    uint32_t first = 0;
+    for (uint32_t q = 0; q < d; ++q) first += (n_buckets - q + n - 1) / n;
+    const float* src = slabs + (size_t)(first + i) * tile_floats;
+    float* dst = by_id + (size_t)b * tile_floats;
+    for (uint32_t k = threadIdx.x; k < tile_floats; k += blockDim.x) dst[k] = src[k];
+}
+
+void merge_stats(nart_render_stats& out, const nart_render_stats& s) {
+    // device times: the slowest device (the devices run concurrently); work counts: summed
+    out.kernel_ms = std::max(out.kernel_ms, s.kernel_ms);
+    out.splat_ms = std::max(out.splat_ms, s.splat_ms);
+    out.latin_ms = std::max(out.latin_ms, s.latin_ms);
+    out.primary_ms = std::max(out.primary_ms, s.primary_ms);
+    out.kernel_launches += s.kernel_launches;
+    out.samples += s.samples;
+    out.traced_samples += s.traced_samples;
+    out.rays_extend += s.rays_extend;
+    out.rays_shadow += s.rays_shadow;
+    out.node_visits += s.node_visits;
+    out.tri_tests += s.tri_tests;
+    out.bounces += s.bounces;
+    out.octree_checks += s.octree_checks;
+    out.octree_replays += s.octree_replays;
+}
+
+int ensure_dev(nart_ctx* ctx, int dev, void*& buf, size_t& cap, size_t bytes, const char* what) {
+    if (bytes <= cap) return NART_OK;
+    HIPCHK(hipSetDevice(dev));
+    if (buf) hipFree(buf);
+    buf = nullptr;
+    cap = 0;
+    if (int rc = dmalloc(ctx, &buf, bytes, what)) return rc;
+    cap = bytes;
+    return NART_OK;
+}
+
+// Render(), multi-device: shard, render concurrently, gather to device 0, combine, copy out.
+int render_multi(nart_ctx* ctx, const nart_render_params* p, nart_pixel* image, nart_render_stats* stats) {
+    const uint32_t n = (uint32_t)ctx->subs.size();
+    int rc = check_params(ctx->subs[0], p);
+    if (rc) return fail(ctx, rc, ctx->subs[0]->err);
+    nart_session_geometry g;
+    nart_session_geometry_of(p, &g);
+    const uint32_t nb = g.n_buckets_x * g.n_buckets_y;
+    const size_t tile_floats = (size_t)g.tile_size * g.tile_size * 5;
+    std::vector<std::vector<uint32_t>> ids(n);
+    for (uint32_t d = 0; d < n; ++d) {
+        ids[d] = shard_ids(nb, n, d);
+        const size_t bytes = std::max<size_t>(1, ids[d].size()) * tile_floats * 4;
+        if ((rc = ensure_dev(ctx, ctx->devs[d], ctx->sub_tiles[d], ctx->sub_cap[d], bytes, "device tiles"))) return rc;
+    }
+    const int dev0 = ctx->devs[0];
+    const size_t all_bytes = (size_t)nb * tile_floats * 4;
+    const size_t img_bytes = (size_t)g.total_width * g.total_height * sizeof(nart_pixel);
+    if ((rc = ensure_dev(ctx, dev0, ctx->d_gather, ctx->cap_gather, all_bytes, "gathered tiles")) ||
+        (rc = ensure_dev(ctx, dev0, ctx->d_byid, ctx->cap_byid, all_bytes, "tiles by bucket id")) ||
+        (rc = ensure_dev(ctx, dev0, ctx->d_image, ctx->cap_image, img_bytes, "image")))
+        return rc;
+
+    // 1. every device renders its buckets (one host thread each, like the TBB task group)
+    std::vector<int> rcs(n, NART_OK);
+    std::vector<nart_render_stats> st(n);
+    std::vector<std::thread> th;
+    for (uint32_t d = 0; d < n; ++d) {
+        std::memset(&st[d], 0, sizeof(st[d]));
+        th.emplace_back([&, d] {
+            if (ids[d].empty()) return;
+            if (hipSetDevice(ctx->devs[d]) != hipSuccess) {
+                rcs[d] = NART_E_HIP;
+                return;
+            }
+            rcs[d] = render_buckets(ctx->subs[d], p, ids[d].data(), (uint32_t)ids[d].size(),
+                                    static_cast<float*>(ctx->sub_tiles[d]), ctx->streams[d], &st[d]);
+            if (rcs[d] == NART_OK && hipStreamSynchronize(ctx->streams[d]) != hipSuccess) rcs[d] = NART_E_HIP;
+        });
+    }
+    for (auto& t : th) t.join();
+    for (uint32_t d = 0; d < n; ++d)
+        if (rcs[d] != NART_OK)
+            return fail(ctx, rcs[d], "device " + std::to_string(ctx->devs[d]) + ": " + ctx->subs[d]->err);
+
+    // 2. gather the slabs to device 0 (rank order), RCCL over xGMI or device copies
+    std::vector<size_t> first(n, 0);
+    for (uint32_t d = 1; d < n; ++d) first[d] = first[d - 1] + ids[d - 1].size();
+    float* slabs = static_cast<float*>(ctx->d_gather);
+    hipStream_t s0 = ctx->streams[0];
+    if (ctx->gather_rccl) {
+        const RcclApi& R = rccl_api();
+        RCCLCHK(R.GroupStart());
+        for (uint32_t d = 0; d < n; ++d) {
+            if (ids[d].empty()) continue;
+            const size_t cnt = ids[d].size() * tile_floats;
+            RCCLCHK(R.Send(ctx->sub_tiles[d], cnt, ncclFloat32, 0, ctx->comms[d], ctx->streams[d]));
+            RCCLCHK(R.Recv(slabs + first[d] * tile_floats, cnt, ncclFloat32, (int)d, ctx->comms[0], s0));
+        }
+        RCCLCHK(R.GroupEnd());
+        for (uint32_t d = 1; d < n; ++d) {
+            HIPCHK(hipSetDevice(ctx->devs[d]));
+            HIPCHK(hipStreamSynchronize(ctx->streams[d]));
+        }
+        HIPCHK(hipSetDevice(dev0));
+    } else {
+        HIPCHK(hipSetDevice(dev0));
+        for (uint32_t d = 0; d < n; ++d)
+            if (!ids[d].empty())
+                HIPCHK(hipMemcpyPeerAsync(slabs + first[d] * tile_floats, dev0, ctx->sub_tiles[d], ctx->devs[d],
+                                          ids[d].size() * tile_floats * 4, s0));
+    }
+
+    // 3. bucket-id order, raster-order combine on device 0, image to the host
+    hipLaunchKernelGGL(k_unshard, dim3(nb), dim3(256), 0, s0, slabs, static_cast<float*>(ctx->d_byid), nb, n,
+                       (uint32_t)tile_floats);
+    HIPCHK(hipGetLastError());
+    if ((rc = nart_hip_combine_async(ctx->subs[0], p, static_cast<const nart_pixel*>(ctx->d_byid),
+                                     static_cast<nart_pixel*>(ctx->d_image), s0)))
+        return fail(ctx, rc, ctx->subs[0]->err);
+    HIPCHK(hipMemcpyAsync(image, ctx->d_image, img_bytes, hipMemcpyDeviceToHost, s0));
+    HIPCHK(hipStreamSynchronize(s0));
+    if (stats)
+        for (uint32_t d = 0; d < n; ++d) merge_stats(*stats, st[d]);
+    return NART_OK;
+}
+
+}  // namespace

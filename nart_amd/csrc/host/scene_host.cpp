@@ -129,26 +129,49 @@ struct TokenReader {
         tok = s.substr(b, p - b);
         return true;
     }
+    // `std::istream >> uint32_t` / `>> float` as libstdc++'s num_get extracts them: skip white
+    // space, then take the longest prefix that fits the number's grammar -- NOT the whole
+    // white-space-delimited token.  "0.418112" read as an integer gives 0 and leaves ".418112",
+    // whose next integer read fails (teapot.geo's UV section: scene.cpp:179-205 then decides the
+    // mesh has no UVs).
+    void skip_ws() {
+        while (p < s.size() && std::isspace(static_cast<unsigned char>(s[p]))) ++p;
+    }
+    static bool digit(char c) { return c >= '0' && c <= '9'; }
     bool u32(uint32_t& v) {
-        size_t save = p;
-        std::string t;
-        if (!next(t)) return false;
-        char* end = nullptr;
-        errno = 0;
-        unsigned long x = std::strtoul(t.c_str(), &end, 10);
-        if (end == t.c_str() || errno || t[0] == '-' || x > 0xFFFFFFFFul) {
-            p = save;
-            return false;
+        skip_ws();
+        bool neg = false;
+        if (p < s.size() && (s[p] == '+' || s[p] == '-')) neg = s[p++] == '-';
+        const size_t b = p;
+        uint64_t x = 0;
+        bool overflow = false;
+        while (p < s.size() && digit(s[p])) {
+            x = x * 10 + (uint64_t)(s[p++] - '0');
+            if (x > 0xFFFFFFFFull) overflow = true, x = 0xFFFFFFFFull;
         }
-        v = static_cast<uint32_t>(x);
+        if (p == b || overflow) return false;  // failbit (no digits / out of range)
+        v = neg ? (uint32_t)(0u - (uint32_t)x) : (uint32_t)x;  // num_get negates unsigned values
         return true;
     }
     bool f32(float& v) {
-        std::string t;
-        if (!next(t)) return false;
+        skip_ws();
+        const size_t b = p;
+        if (p < s.size() && (s[p] == '+' || s[p] == '-')) ++p;
+        bool any = false;
+        while (p < s.size() && digit(s[p])) ++p, any = true;
+        if (p < s.size() && s[p] == '.') {
+            ++p;
+            while (p < s.size() && digit(s[p])) ++p, any = true;
+        }
+        if (any && p < s.size() && (s[p] == 'e' || s[p] == 'E')) {
+            ++p;
+            if (p < s.size() && (s[p] == '+' || s[p] == '-')) ++p;
+            while (p < s.size() && digit(s[p])) ++p;
+        }
+        const std::string t = s.substr(b, p - b);
         char* end = nullptr;
-        v = std::strtof(t.c_str(), &end);  // libstdc++ num_get<float> -> strtof
-        return end != t.c_str();
+        v = std::strtof(t.c_str(), &end);  // num_get<float> -> __convert_to_v -> strtof
+        return !t.empty() && end == t.c_str() + t.size();
     }
 };
 

@@ -2,8 +2,10 @@
 // build, light precomputation) and the Render()-equivalent launch sequence.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rccl/rccl.h>  // types only: RCCL is loaded at run time by the multi-device context
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -84,6 +86,17 @@ struct nart_ctx {
     void* d_sort_tmp = nullptr;
     size_t cap_sort_tmp = 0;
     uint32_t cap_queue = 0;
+    // multi-device context (nart_hip_create_multi, host/multi_gpu.h): one single-device
+    // sub-context per listed device; device 0 gathers and combines
+    std::vector<nart_ctx*> subs;
+    std::vector<int> devs;
+    std::vector<hipStream_t> streams;
+    std::vector<void*> sub_tiles;
+    std::vector<size_t> sub_cap;
+    std::vector<ncclComm_t> comms;
+    bool gather_rccl = false;
+    void *d_gather = nullptr, *d_byid = nullptr, *d_image = nullptr;
+    size_t cap_gather = 0, cap_byid = 0, cap_image = 0;
 };
 
 namespace {
@@ -373,6 +386,11 @@ uint32_t render_lds_nodes(const nart_ctx* ctx, size_t fixed = 0, uint32_t blocks
     return (uint32_t)std::min<size_t>(n, ctx->num_nodes);
 }
 
+// The ray-queue kernel's fixed LDS (stack + outboxes + results + id rings) fits one block per CU.
+bool rq_fits(const nart_ctx* ctx) {
+    return rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK) <= (size_t)160 * 1024;
+}
+
 // ---------------------------------------------------------------- megakernel scheduling
 // A pixel's samples are one serial chain (its RNG stream), so a frame can finish no earlier
 // than its costliest pixels, and a wave of 64 costly pixels runs several times longer than one
@@ -496,16 +514,20 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     auto kern = k_render<MAXL, COUNT, ENV, false>;
     auto kern_q = k_render<MAXL, COUNT, ENV, true>;
     auto kern_rq = k_render_rq<MAXL, COUNT, ENV>;
-    static bool attr = false;  // dynamic LDS above the 64 KiB default
-    if (!attr) {
+    static std::atomic<uint64_t> attr{0};  // dynamic LDS above the 64 KiB default, set once per device
+    const uint64_t dbit = 1ull << (ctx->device & 63);
+    if (!(attr.load() & dbit)) {
         for (const void* f : {(const void*)kern, (const void*)kern_q, (const void*)k_render<MAXL, true, ENV, false>,
                               (const void*)kern_rq, (const void*)k_primary<COUNT, ENV>})
             hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
+        attr.fetch_or(dbit);
     }
     // variant 0: ray-queue kernel; 2: k_render with the traversal quorum on every launch;
-    // 3: k_render with the quorum chosen by rounds of resident waves (the previous default)
-    const bool rq = ctx->variant == 0;
+    // 3: k_render with the quorum chosen by rounds of resident waves (the previous default).
+    // The ray-queue kernel's 512-lane blocks keep a stack_depth * 4 KiB traversal stack plus
+    // 60 KiB of ray outboxes in LDS: a BVH deeper than 24 levels does not fit, and those scenes
+    // run k_render (256-lane blocks, stack_depth * 2 KiB) instead -- same image.
+    const bool rq = ctx->variant == 0 && rq_fits(ctx);
     // camera rays first, coherently (k_primary); NART_PRIMARY=0 leaves them to the path kernel
     static const bool primary = !std::getenv("NART_PRIMARY") || std::atoi(std::getenv("NART_PRIMARY")) != 0;
 
@@ -562,7 +584,8 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     if (mode > 0) {
         if (blocks > resident) {  // more pixels than resident lanes: persistent grid + queue
             const uint32_t n = a.n_slots;
-            int rc = ensure_queue(ctx, n + 32u * W);  // room for the speculative pairs' duplicates
+            // room for the speculative groups' duplicates: qlen = n + (Q - 1) * k * W with Q * k <= 64
+            int rc = ensure_queue(ctx, n + 63u * W);
             if (rc) return rc;
             const dim3 eg((n + 255) / 256);
             // costly pixels per first-round wave: few when the shard is small (their serial chains
@@ -1038,13 +1061,16 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
 #define NART_SPLAT_NP 4
 #endif
         const uint64_t n4 = (uint64_t)nbk * g.tile_size * ((g.tile_size + NART_SPLAT_NP - 1) / NART_SPLAT_NP);
-        // mode 4 (default): bucket per block, samples staged through LDS in source-row chunks of cw
-        // columns (NART_SPLAT_CHUNK_KB of LDS per block)
+        // mode 4 (selectable; mode 3 is the default): bucket per block, samples staged through LDS
+        // in source-row chunks of cw columns (NART_SPLAT_CHUNK_KB of LDS per block)
         static const size_t chunk_kb =
             std::getenv("NART_SPLAT_CHUNK_KB") ? std::strtoull(std::getenv("NART_SPLAT_CHUNK_KB"), nullptr, 10) : 48;
         const size_t col_bytes = (size_t)p->spp * (sizeof(float4) + sizeof(float2));
         const uint32_t cw = (uint32_t)std::min<size_t>(p->bucket_size, std::max<size_t>(1, chunk_kb * 1024 / col_bytes));
-        static const uint32_t lblk = std::getenv("NART_SPLAT_LDS_BLOCK") ? (uint32_t)std::atoi(std::getenv("NART_SPLAT_LDS_BLOCK")) : 256u;
+        // k_splat_lds is declared __launch_bounds__(256): larger blocks would not launch
+        static const uint32_t lblk = std::getenv("NART_SPLAT_LDS_BLOCK")
+                                         ? (uint32_t)std::max(64, std::min(256, std::atoi(std::getenv("NART_SPLAT_LDS_BLOCK"))))
+                                         : 256u;
         const uint32_t nt = (tpx + lblk - 1) / lblk;
         const int lmode = sa.thr ? (sa.invB != 0.f ? 2 : 1) : 0;
         if (splat_mode >= 4 && nt <= 4 && (size_t)cw * col_bytes <= (size_t)159 * 1024) {
@@ -1177,6 +1203,8 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
 }
 
 }  // namespace
+
+#include "host/multi_gpu.h"
 
 extern "C" {
 
@@ -1339,8 +1367,9 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     std::memcpy(S.cam_m, blob->camera.m, sizeof(S.cam_m));
     // glm::tan(glm::radians(fov)) with the host libm, as the reference (pinholecamera.cpp:20)
     S.cam_tan = std::tan(blob->camera.fov * (float)0.01745329251994329576923690768489);
-    // reference octree + replay heap pool: one slot per 32 resident lanes (a slot is held only
-    // while a lane replays), at least 4096 and within 256 MiB
+    // reference octree + replay heap pool: entries of 64 heaps (one per lane of a replaying
+    // wave, octree.h oc_replay), held only while a wave replays; up to 512 entries within 256 MiB
+    // (NART_OC_POOL overrides the count: tests force a single entry)
     if ((rc = upload(ctx, ctx->d_oc_nodes, oct.nodes.data(), oct.nodes.size()))) return bail(rc);
     if ((rc = upload(ctx, ctx->d_oc_chunks, oct.chunks.data(), oct.chunks.size()))) return bail(rc);
     if ((rc = upload(ctx, ctx->d_oc_tris, oct.tris.data(), oct.tris.size()))) return bail(rc);
@@ -1351,13 +1380,15 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     S.tri_leaf = (const int32_t*)ctx->d_tri_leaf;
     S.oc_root = oct.root;
     S.oc_cap = (uint32_t)std::max<size_t>(oct.nodes.size(), 1);
-    S.oc_pool = (uint32_t)std::max<size_t>(64, std::min<size_t>(4096, (256ull << 20) / (8ull * S.oc_cap)));
+    S.oc_pool = (uint32_t)std::max<size_t>(1, std::min<size_t>(512, (256ull << 20) / (64ull * 8ull * S.oc_cap)));
+    if (const char* v = std::getenv("NART_OC_POOL")) S.oc_pool = (uint32_t)std::max(1, std::atoi(v));
     S.oc_scale = maxabs;
     S.oc_exact = 1;
-    if (const char* v = std::getenv("NART_OCTREE_EXACT")) S.oc_exact = std::atoi(v) != 0;
+    // NART_OCTREE_EXACT: 0 off (A/B timing only), 2 every query replays the octree search (tests)
+    if (const char* v = std::getenv("NART_OCTREE_EXACT")) S.oc_exact = std::max(0, std::min(2, std::atoi(v)));
     if (hipMalloc(&ctx->d_oc_lock, sizeof(uint32_t) * S.oc_pool) != hipSuccess ||
         hipMemset(ctx->d_oc_lock, 0, sizeof(uint32_t) * S.oc_pool) != hipSuccess ||
-        hipMalloc(&ctx->d_oc_heap, sizeof(unsigned long long) * S.oc_pool * S.oc_cap) != hipSuccess)
+        hipMalloc(&ctx->d_oc_heap, sizeof(unsigned long long) * 64 * S.oc_pool * S.oc_cap) != hipSuccess)
         return bail(NART_E_OOM);
     S.oc_lock = (uint32_t*)ctx->d_oc_lock;
     S.oc_heap = (unsigned long long*)ctx->d_oc_heap;
@@ -1367,6 +1398,22 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
 
 void nart_hip_destroy(nart_ctx* ctx) {
     if (!ctx) return;
+    if (!ctx->subs.empty()) {  // multi-device context
+        const RcclApi& R = rccl_api();
+        for (ncclComm_t c : ctx->comms)
+            if (c && R.ok) R.CommDestroy(c);
+        for (size_t d = 0; d < ctx->subs.size(); ++d) {
+            hipSetDevice(ctx->devs[d]);
+            if (d < ctx->sub_tiles.size() && ctx->sub_tiles[d]) hipFree(ctx->sub_tiles[d]);
+            if (d < ctx->streams.size() && ctx->streams[d]) hipStreamDestroy(ctx->streams[d]);
+        }
+        hipSetDevice(ctx->devs[0]);
+        for (void* b : {ctx->d_gather, ctx->d_byid, ctx->d_image})
+            if (b) hipFree(b);
+        for (nart_ctx* c : ctx->subs) nart_hip_destroy(c);
+        delete ctx;
+        return;
+    }
     hipSetDevice(ctx->device);
     void* bufs[] = {ctx->d_nodes, ctx->d_tri_isect, ctx->d_tri_perm, ctx->d_tris, ctx->d_tri_mesh, ctx->d_meshes, ctx->d_mats,
                     ctx->d_lights, ctx->d_texs, ctx->d_tex_pool, ctx->d_slot_xy, ctx->d_slot_so, ctx->d_rng, ctx->d_samples, ctx->d_prim,
@@ -1391,11 +1438,14 @@ const char* nart_hip_last_error(const nart_ctx* ctx) { return ctx ? ctx->err.c_s
 int nart_hip_set_counters(nart_ctx* ctx, int enable) {
     if (!ctx) return NART_E_INVALID;
     ctx->counters = enable != 0;
+    for (nart_ctx* c : ctx->subs) c->counters = ctx->counters;
     return NART_OK;
 }
 
 int nart_hip_set_splat_mode(nart_ctx* ctx, int mode) {
     if (!ctx) return NART_E_INVALID;
+    for (nart_ctx* c : ctx->subs)
+        if (int rc = nart_hip_set_splat_mode(c, mode)) return fail(ctx, rc, c->err);
     if (mode < 0 || mode > 4)
         return fail(ctx, NART_E_UNSUPPORTED, "splat mode must be 0-4 (4 LDS-staged, 3 four pixels per lane, 2-0 one "
                                              "pixel per lane)");
@@ -1405,6 +1455,8 @@ int nart_hip_set_splat_mode(nart_ctx* ctx, int mode) {
 
 int nart_hip_set_variant(nart_ctx* ctx, int variant) {
     if (!ctx) return NART_E_INVALID;
+    for (nart_ctx* c : ctx->subs)
+        if (int rc = nart_hip_set_variant(c, variant)) return fail(ctx, rc, c->err);
     if (variant < 0 || variant > 3)
         return fail(ctx, NART_E_UNSUPPORTED, "variant must be 0 (megakernel with a wave ray queue), 1 (wavefront), 2 "
                                              "(megakernel, traversal quorum always) or 3 (megakernel, quorum by rounds)");
@@ -1415,6 +1467,8 @@ int nart_hip_set_variant(nart_ctx* ctx, int variant) {
 int nart_hip_render_buckets_async(nart_ctx* ctx, const nart_render_params* p, const uint32_t* bucket_ids,
                                   uint32_t n_buckets, nart_pixel* d_tiles, void* stream, nart_render_stats* stats) {
     if (!ctx || !bucket_ids || !d_tiles) return NART_E_INVALID;
+    if (!ctx->subs.empty())
+        return fail(ctx, NART_E_UNSUPPORTED, "render_buckets_async takes a single-device context (one per rank)");
     auto t0 = std::chrono::steady_clock::now();
     int rc = render_buckets(ctx, p, bucket_ids, n_buckets, reinterpret_cast<float*>(d_tiles), (hipStream_t)stream, stats);
     if (stats) stats->render_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1424,6 +1478,7 @@ int nart_hip_render_buckets_async(nart_ctx* ctx, const nart_render_params* p, co
 int nart_hip_combine_async(nart_ctx* ctx, const nart_render_params* p, const nart_pixel* d_tiles, nart_pixel* d_image,
                            void* stream) {
     if (!ctx || !p || !d_tiles || !d_image) return NART_E_INVALID;
+    if (!ctx->subs.empty()) return nart_hip_combine_async(ctx->subs[0], p, d_tiles, d_image, stream);
     HIPCHK(hipSetDevice(ctx->device));
     nart_session_geometry g;
     nart_session_geometry_of(p, &g);
@@ -1448,6 +1503,11 @@ int nart_hip_combine_async(nart_ctx* ctx, const nart_render_params* p, const nar
 int nart_hip_render(nart_ctx* ctx, const nart_render_params* p, nart_pixel* image, nart_render_stats* stats) {
     if (!ctx || !p || !image) return NART_E_INVALID;
     auto t0 = std::chrono::steady_clock::now();
+    if (!ctx->subs.empty()) {
+        const int rc = render_multi(ctx, p, image, stats);
+        if (stats) stats->render_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        return rc;
+    }
     int rc = check_params(ctx, p);
     if (rc) return rc;
     HIPCHK(hipSetDevice(ctx->device));
@@ -1477,6 +1537,10 @@ int nart_hip_render(nart_ctx* ctx, const nart_render_params* p, nart_pixel* imag
 int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t x0, uint32_t y0, uint32_t w,
                             uint32_t h, float* out) {
     if (!ctx || !p || !out) return NART_E_INVALID;
+    if (!ctx->subs.empty()) {  // per-sample debugging runs on the first device
+        const int rc = nart_hip_render_samples(ctx->subs[0], p, x0, y0, w, h, out);
+        return rc ? fail(ctx, rc, ctx->subs[0]->err) : NART_OK;
+    }
     int rc = check_params(ctx, p);
     if (rc) return rc;
     HIPCHK(hipSetDevice(ctx->device));
@@ -1516,10 +1580,13 @@ int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t
     ra.counters = ctx->d_counters;
     rc = launch_latin(ctx, ra, 0);
     if (rc) return rc;
+#ifdef NART_DEVPROBE
+    // development probe of the speculative pairs (tools/pair_latency.py; build with
+    // NART_HIP_DEFINES=-DNART_DEVPROBE): every pixel of the rect on two or four lanes
     if (std::getenv("NART_SAMPLES_PAIRS") && std::atoi(std::getenv("NART_SAMPLES_PAIRS")) && ctx->variant == 0 &&
         p->integrator == NART_INTEGRATOR_PATH && n <= 65536) {
-        // development probe of the speculative pairs: every pixel of the rect on two lanes
-        // (the ray-queue kernel alone, camera rays included; no work queue refill)
+        if (ctx->has_env || p->bounces > 10) return fail(ctx, NART_E_UNSUPPORTED, "pairs probe: glass-like scenes only");
+        // the ray-queue kernel alone, camera rays included; no work queue refill
         const uint32_t Q = std::atoi(std::getenv("NART_SAMPLES_PAIRS")) >= 4 ? 4u : 2u;  // lanes per pixel
         rc = ensure_queue(ctx, Q * n);
         if (rc) return rc;
@@ -1540,11 +1607,12 @@ int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t
             hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             attr = true;
         }
-        if (ctx->has_env || p->bounces > 10) return fail(ctx, NART_E_UNSUPPORTED, "pairs probe: glass-like scenes only");
         hipLaunchKernelGGL(kern, dim3((Q * n + NART_RQ_BLOCK - 1) / NART_RQ_BLOCK), dim3(NART_RQ_BLOCK), lds_rq, 0,
                            ctx->scene, r2);
         HIPCHK(hipGetLastError());
-    } else {
+    } else
+#endif
+    {
         rc = dispatch_render(ctx, ra, p->integrator, 0);
         if (rc) return rc;
     }
@@ -1586,6 +1654,7 @@ int nart_hip_splat_thresholds(float filter_width, float* thr65) {
 
 int nart_hip_eval_sincos(nart_ctx* ctx, const float* x, uint32_t n, float* s, float* c) {
     if (!ctx || !x || !s || !c) return NART_E_INVALID;
+    if (!ctx->subs.empty()) return nart_hip_eval_sincos(ctx->subs[0], x, n, s, c);
     HIPCHK(hipSetDevice(ctx->device));
     float *dx = nullptr, *ds = nullptr, *dc = nullptr;
     HIPCHK(hipMalloc(&dx, (size_t)n * 4 + 4));
@@ -1599,6 +1668,91 @@ int nart_hip_eval_sincos(nart_ctx* ctx, const float* x, uint32_t n, float* s, fl
     hipFree(dx);
     hipFree(ds);
     hipFree(dc);
+    return NART_OK;
+}
+
+int nart_hip_device_count(int* count) {
+    if (!count) return NART_E_INVALID;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        *count = 0;
+        return NART_E_HIP;
+    }
+    *count = n;
+    return NART_OK;
+}
+
+int nart_hip_shard_buckets(uint32_t n_buckets, uint32_t n_devices, uint32_t device_index, uint32_t* ids,
+                           uint32_t* count) {
+    if (!count || !n_devices || device_index >= n_devices) return NART_E_INVALID;
+    const std::vector<uint32_t> v = shard_ids(n_buckets, n_devices, device_index);
+    if (ids) std::memcpy(ids, v.data(), v.size() * sizeof(uint32_t));
+    *count = (uint32_t)v.size();
+    return NART_OK;
+}
+
+int nart_hip_create_multi(const nart_scene_blob* blob, const int* device_ids, int n_devices, nart_ctx** out) {
+    if (!blob || !out || !device_ids || n_devices < 1 || n_devices > 64) return NART_E_INVALID;
+    *out = nullptr;
+    const char* gm = std::getenv("NART_GATHER");
+    const bool force_rccl = gm && std::string(gm) == "rccl";
+    const bool force_copy = gm && std::string(gm) == "copy";
+    if (n_devices == 1 && !force_rccl) return nart_hip_create(blob, device_ids[0], out);
+    nart_ctx* ctx = new (std::nothrow) nart_ctx();
+    if (!ctx) return NART_E_OOM;
+    ctx->device = device_ids[0];
+    auto bail = [&](int code) {
+        nart_hip_destroy(ctx);
+        return code;
+    };
+    bool distinct = true;
+    for (int i = 0; i < n_devices; ++i)
+        for (int j = 0; j < i; ++j) distinct = distinct && device_ids[i] != device_ids[j];
+    for (int d = 0; d < n_devices; ++d) {
+        nart_ctx* sub = nullptr;
+        if (int rc = nart_hip_create(blob, device_ids[d], &sub)) return bail(rc);
+        ctx->subs.push_back(sub);
+        ctx->devs.push_back(device_ids[d]);
+        ctx->sub_tiles.push_back(nullptr);
+        ctx->sub_cap.push_back(0);
+        hipStream_t st = nullptr;
+        if (hipSetDevice(device_ids[d]) != hipSuccess || hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess)
+            return bail(NART_E_HIP);
+        ctx->streams.push_back(st);
+    }
+    ctx->gather_rccl = force_rccl || (distinct && !force_copy);
+    if (ctx->gather_rccl) {
+        const RcclApi& R = rccl_api();
+        if (!R.ok || !distinct) {
+            const int rc = NART_E_RCCL;
+            nart_hip_destroy(ctx);
+            return rc;
+        }
+        ctx->comms.assign(n_devices, nullptr);
+        if (R.CommInitAll(ctx->comms.data(), n_devices, device_ids) != ncclSuccess) {
+            ctx->comms.clear();
+            return bail(NART_E_RCCL);
+        }
+    } else {
+        // device copies to device 0 (peer access where the devices differ)
+        hipSetDevice(device_ids[0]);
+        for (int d = 1; d < n_devices; ++d)
+            if (device_ids[d] != device_ids[0]) {
+                int can = 0;
+                if (hipDeviceCanAccessPeer(&can, device_ids[0], device_ids[d]) == hipSuccess && can)
+                    hipDeviceEnablePeerAccess(device_ids[d], 0);
+                (void)hipGetLastError();  // already enabled is fine
+            }
+    }
+    *out = ctx;
+    return NART_OK;
+}
+
+int nart_hip_context_devices(const nart_ctx* ctx, int* n_devices, int* uses_rccl) {
+    if (!ctx || !n_devices) return NART_E_INVALID;
+    *n_devices = ctx->subs.empty() ? 1 : (int)ctx->subs.size();
+    if (uses_rccl) *uses_rccl = ctx->gather_rccl ? 1 : 0;
     return NART_OK;
 }
 

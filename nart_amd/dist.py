@@ -10,9 +10,56 @@ tiles into the image in bucket raster order (render.cpp:152-203).  Across ranks:
   * rank 0 scatters them into bucket-id order and combines in bucket raster order, so the
     image is bit-identical for any N.
 No other collective is on the data path.
+
+spawn_ranks starts the one-process-per-GPU job itself when a script is run with --gpus N and no
+launcher (torch.distributed.run) set up the rendezvous: N children with RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT, started before the parent touches any GPU.
 """
+import os
+import socket
+import subprocess
+import sys
+import time
+
 import numpy as np
 import torch
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n, argv, env=None):
+    """Run `python argv...` as ranks 0..n-1 of one job (rendezvous on 127.0.0.1) and return the
+    first non-zero exit code, or 0.  If a rank fails, the ranks still running are stopped (they
+    would wait for it at the next collective)."""
+    port = free_port()
+    base = dict(os.environ if env is None else env)
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable] + list(argv), env=e))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in live:  # exact children of this call, never a pattern
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
 
 
 class BucketShard:

@@ -86,3 +86,27 @@ def test_bvh_depth_cap(built, glass_scene, monkeypatch):
         capped = nart_amd.bvh_info(glass_scene)
         assert capped["num_leaf_tris"] == 2560
         assert capped["stack_depth"] <= md + math.ceil(math.log2(2560 / 4)) + 2, (md, capped)
+
+
+def test_multi_device_shard_partition(built):
+    """nart_hip_shard_buckets (host only): the multi-device context's buckets per device partition
+    the frame (every bucket exactly once, ascending per device, b % n == device)."""
+    import numpy as np
+    for nb_, n in [(8160, 8), (15, 2), (7, 4), (3, 8), (32400, 8), (1, 1)]:
+        parts = [nart_amd.shard_buckets(nb_, n, d) for d in range(n)]
+        allb = np.concatenate(parts)
+        assert np.array_equal(np.sort(allb), np.arange(nb_))
+        for d, ids in enumerate(parts):
+            assert np.all(ids % n == d) and np.all(np.diff(ids.astype(np.int64)) > 0)
+
+
+def test_multi_device_create_without_gpu_fails_cleanly(built, glass_scene):
+    import ctypes as C
+    lib = nart_amd.hip_lib()
+    ctx = C.c_void_p()
+    devs = (C.c_int * 2)(0, 1)
+    rc = lib.nart_hip_create_multi(C.c_void_p(glass_scene.blob), devs, 2, C.byref(ctx))
+    assert rc != 0 and not ctx.value
+    cnt = C.c_int(-1)
+    lib.nart_hip_device_count(C.byref(cnt))
+    assert cnt.value == 0

@@ -67,3 +67,27 @@ def test_ranks_on_one_gpu_match_single_rank(gpu, glass_scene, tmp_path, world):
     p.image_width, p.image_height, p.spp = w, h, spp
     ref = nart_amd.HipRenderer(glass_scene).render(p)
     assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
+
+
+def test_bench_spawned_ranks_on_one_gpu(gpu, glass_scene, tmp_path):
+    """bench.py --gpus 2 without a launcher: it spawns both ranks itself (here both on GPU 0 with
+    the gloo backend; the driver's 8-GPU runs use RCCL), reports n_gpus 2, and rank 0's combined
+    image equals the single-rank render bit for bit."""
+    import json
+    import subprocess
+    import nart_amd
+    out = str(tmp_path / "bench_img.npy")
+    env = dict(os.environ, NART_DIST_BACKEND="gloo", NART_BENCH_SAME_DEVICE="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--size", "200x120x8",
+                        "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--dump-image", out],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2
+    img = np.load(out)
+    p = nart_amd.load_sessions(glass_scene.path)[0]
+    p.image_width, p.image_height, p.spp = 200, 120, 8
+    ref = nart_amd.HipRenderer(glass_scene).render(p)
+    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))

@@ -77,3 +77,41 @@ def test_depth_capped_bvh_parity(gpu, glass_scene, monkeypatch):
     r = nart_amd.HipRenderer(glass_scene)
     p = _params(glass_scene, 64, 48, 4)
     assert _bits_equal(r.render(p), oracle.Oracle(glass_scene).render(p))
+
+
+def test_deep_bvh_variant0_falls_back(gpu, tmp_path):
+    """A BVH whose traversal stack (29 levels) exceeds what the 512-lane ray-queue blocks can keep
+    in LDS (24 levels): variant 0 must still render -- on the 256-lane kernel -- and match the
+    oracle (such scenes used to pass create and fail at launch)."""
+    from nart_amd import scenes
+    sc = nart_amd.Scene(scenes.deep_bvh(str(tmp_path)))
+    assert nart_amd.api.bvh_info(sc)["stack_depth"] > 25
+    p = _params(sc, 96, 64, 4)
+    g = nart_amd.HipRenderer(sc, variant=0).render(p)
+    r = oracle.Oracle(sc).render(p)
+    assert _bits_equal(g, r)
+    assert float(np.abs(r[..., :3]).sum()) > 0.0  # geometry and light are visible
+
+
+@pytest.mark.parametrize("variant", [0, 1, 3], ids=["rayqueue", "wavefront", "megakernel"])
+def test_forced_octree_replay_single_pool_entry(gpu, cornell_scene, monkeypatch, variant):
+    """Every query answered by replaying the reference octree search (NART_OCTREE_EXACT=2) with a
+    replay pool of ONE entry (NART_OC_POOL=1): every wave that replays contends for the same
+    heaps.  Lanes of a wave share the entry their lowest lane acquired, so no lane waits on a
+    wave-mate; the frame must complete and equal the oracle's bit for bit."""
+    import torch
+    monkeypatch.setenv("NART_OCTREE_EXACT", "2")
+    monkeypatch.setenv("NART_OC_POOL", "1")
+    r = nart_amd.HipRenderer(cornell_scene, variant=variant)
+    p = _params(cornell_scene, 96, 64, 4)
+    g = nart_amd.session_geometry(p)
+    nb = g.n_buckets_x * g.n_buckets_y
+    ids = np.arange(nb, dtype=np.uint32)
+    tiles = torch.zeros((nb, g.tile_size * g.tile_size, 5), dtype=torch.float32, device="cuda")
+    st = nart_amd.RenderStats()
+    r.set_counters(True)
+    r.render_buckets_async(p, ids, tiles.data_ptr(), torch.cuda.current_stream().cuda_stream, st)
+    torch.cuda.synchronize()
+    ref = oracle.Oracle(cornell_scene).render_buckets(p, ids)
+    assert _bits_equal(tiles.cpu().numpy(), ref)
+    assert st.octree_replays >= st.rays_extend  # every extension query (and shadow query) replayed

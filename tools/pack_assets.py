@@ -55,7 +55,37 @@ def main(ref, scene_name="glassSphere"):
     print("wrote", out, os.path.getsize(out), "bytes")
 
 
+MESHES = ("teapot", "monkey", "cube", "plane")  # C4 assets + ingestion checks
+TEXTURES = ("uv", "noise")                     # C4 rho_d / normal map (ZIPS EXRs, copied as-is)
+
+
+def pack_meshes(ref):
+    """assets/meshes.npz: the reference's loose .geo meshes that no packed scene carries, stored
+    like the scene meshes (token kinds, ints, strtof floats); input/textures/{uv,noise}.exr are
+    copied unchanged to assets/textures/ (data files, read by the drop-in's own EXR reader)."""
+    import shutil
+    arrays = {}
+    for name in MESHES:
+        k, i, f = parse_geo(os.path.join(ref, "input", "meshes", name + ".geo"))
+        arrays["geo_%s.geo_kinds" % name] = k
+        arrays["geo_%s.geo_ints" % name] = i
+        arrays["geo_%s.geo_floats" % name] = f
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets")
+    out = os.path.join(root, "meshes.npz")
+    np.savez_compressed(out, **arrays)
+    print("wrote", out, os.path.getsize(out), "bytes")
+    os.makedirs(os.path.join(root, "textures"), exist_ok=True)
+    for t in TEXTURES:
+        dst = os.path.join(root, "textures", t + ".exr")
+        shutil.copyfile(os.path.join(ref, "input", "textures", t + ".exr"), dst)
+        print("copied", dst, os.path.getsize(dst), "bytes")
+
+
 if __name__ == "__main__":
     ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
-    for name in (sys.argv[2:] or ["glassSphere"]):
-        main(ref, name)
+    names = sys.argv[2:] or ["glassSphere"]
+    for name in names:
+        if name == "meshes":
+            pack_meshes(ref)
+        else:
+            main(ref, name)
