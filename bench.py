@@ -48,9 +48,15 @@ CONFIGS = {
     "c2": dict(scene=lambda d: scenes.cornell(d), w=1920, h=1080, spp=64, stride=29,
                workload="C2 synthesized Lambert Cornell box, one disk light, 1920x1080 64spp, bounces 10",
                data="synthesized scene (nart_amd/scenes.py cornell)"),
-    "c4": dict(scene=lambda d: scenes.environment(d), w=3840, h=2160, spp=512, stride=211,
-               workload="C4-style environment-lit textured, normal-mapped plastic + rough glass, 3840x2160 512spp",
-               data="synthesized scene + generated sky EXR (nart_amd/scenes.py environment)"),
+    "c4": dict(scene=lambda d: scenes.c4_teapot(d), w=3840, h=2160, spp=512, stride=211,
+               workload="C4 reference teapot.geo (15,704 triangles) as plastic with input/textures/uv.exr rho_d and "
+                        "noise.exr normal map on a lambert plane.geo, generated 1024x512 environment light, "
+                        "3840x2160 512spp",
+               data="reference meshes/textures packed in assets/ + generated sky EXR (nart_amd/scenes.py c4_teapot)"),
+    "c4env": dict(scene=lambda d: scenes.environment(d), w=3840, h=2160, spp=512, stride=211,
+                  workload="C4-style environment-lit textured, normal-mapped plastic + rough glass (UV spheres), "
+                           "3840x2160 512spp (round-2 C4 scene)",
+                  data="synthesized scene + generated sky EXR (nart_amd/scenes.py environment)"),
     "c5": dict(scene=lambda d: scenes.volume(d, kind="c5"), w=1920, h=1080, spp=1024, stride=59,
                workload="C5 homogeneous medium (density 1, sigma_s 8), volume integrator, 1920x1080 1024spp, 32 bounces",
                data="synthesized .vol + generated sky EXR (nart_amd/scenes.py volume)"),

@@ -386,9 +386,14 @@ uint32_t render_lds_nodes(const nart_ctx* ctx, size_t fixed = 0, uint32_t blocks
     return (uint32_t)std::min<size_t>(n, ctx->num_nodes);
 }
 
-// The ray-queue kernel's fixed LDS (stack + outboxes + results + id rings) fits one block per CU.
+// The ray-queue kernel's fixed LDS (stack + outboxes + results + id rings) fits one block per CU
+// (stack_depth <= 24 at 512 lanes).  NART_RQ_LDS_LIMIT lowers the budget (tests of the fallback).
 bool rq_fits(const nart_ctx* ctx) {
-    return rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK) <= (size_t)160 * 1024;
+    const size_t limit = std::getenv("NART_RQ_LDS_LIMIT")
+                                    ? std::min<size_t>(std::strtoull(std::getenv("NART_RQ_LDS_LIMIT"), nullptr, 10),
+                                                       (size_t)160 * 1024)
+                                    : (size_t)160 * 1024;
+    return rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK) <= limit;
 }
 
 // ---------------------------------------------------------------- megakernel scheduling

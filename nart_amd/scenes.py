@@ -355,41 +355,6 @@ def volume(directory=None, width=320, height=180, spp=16, kind="c5"):
     return path
 
 
-def deep_bvh(directory=None, width=96, height=64, spp=4, n_tris=200, ratio=0.8):
-    """A BVH far deeper than the ray-queue kernel's LDS stack allows at 512 lanes (> 24 levels):
-    a string of triangles shrinking geometrically towards a point, so every SAH split peels off
-    one triangle, in front of a Lambert backdrop under a disk light.  Exercises the fallback of
-    variant 0 to the 256-lane kernel (render.hip rq_fits)."""
-    d = directory or tempfile.mkdtemp(prefix="nart_deep_")
-    os.makedirs(d, exist_ok=True)
-    verts, faces = [], []
-    for k in range(n_tris):
-        s = ratio ** k
-        c = np.array([1.2 * s, 0.0, 0.3 * s])  # converges to the origin: no precision collapse
-        a = 0.9 * k
-        e1 = np.array([np.cos(a), 0.25, np.sin(a)]) * 0.45 * s
-        e2 = np.array([-np.sin(a), -0.3, np.cos(a)]) * 0.45 * s
-        base = len(verts)
-        verts += [tuple(c), tuple(c + e1), tuple(c + e2)]
-        faces.append([base, base + 1, base + 2])
-    write_geo(os.path.join(d, "string.geo"), faces, verts, [(0.0, -1.0, 0.0)], [[0, 0, 0] for _ in faces])
-    write_geo(os.path.join(d, "back.geo"), *_grid_quad((-2, 1.5, -1), (4, 0, 0), (0, 0, 3), (0, -1, 0), 2))
-    scene = {
-        "renderSessions": [{"imageWidth": width, "imageHeight": height, "bucketSize": 16, "spp": spp, "bounces": 6,
-                            "filterWidth": 2, "rougheningFactor": 0.1}],
-        "camera": {"fov": 20.0, "transform": [1, 0, 0, 0.4, 0, 0, -1, -4.0, 0, 1, 0, 0.2, 0, 0, 0, 1]},
-        "meshes": [{"filePath": os.path.join(d, "string.geo"),
-                    "material": {"type": "glass", "rho_s": [1, 1, 1], "tau": [1, 1, 1], "eta": 1.4, "roughness": 0.05}},
-                   {"filePath": os.path.join(d, "back.geo"), "material": {"type": "lambert", "rho_d": [0.6, 0.6, 0.6]}}],
-        "lights": [{"type": "disk", "radius": 0.6, "Le": [1, 1, 1], "intensity": 30.0,
-                    "transform": [1, 0, 0, 0, 0, 1, 0, -1.0, 0, 0, 1, 2.5, 0, 0, 0, 1]}],
-    }
-    path = os.path.join(d, "deep.json")
-    with open(path, "w") as f:
-        json.dump(scene, f, indent=1)
-    return path
-
-
 def reference_mesh(name, directory):
     """Materialise one of the reference's loose meshes (assets/meshes.npz: teapot, monkey, cube,
     plane; tools/pack_assets.py) as `directory/<name>.geo`; returns the path."""
@@ -407,11 +372,28 @@ def reference_texture(name):
     return os.path.join(ASSETS, "textures", name + ".exr")
 
 
+def tangent_normal_map(n=1024, amp=0.35):
+    """Tangent-space normal map of a smooth height field (fixed formula, no RNG), encoded as
+    (normal + 1) / 2; every normal has z > 0.49, so no texel decodes to a zero vector."""
+    v, u = np.mgrid[0:n, 0:n].astype(np.float64)
+    u, v = (u + 0.5) / n, (v + 0.5) / n
+    dhu = amp * 2 * np.pi * 8 * np.cos(2 * np.pi * 8 * u) * np.cos(2 * np.pi * 6 * v) * 0.1
+    dhv = -amp * 2 * np.pi * 6 * np.sin(2 * np.pi * 8 * u) * np.sin(2 * np.pi * 6 * v) * 0.1
+    nrm = np.stack([-dhu, -dhv, np.ones_like(u)], -1)
+    nrm /= np.linalg.norm(nrm, axis=-1, keepdims=True)
+    rgb = (nrm + 1.0) * 0.5
+    return np.concatenate([rgb, np.ones_like(u)[..., None]], -1).astype(np.float32)
+
+
 def c4_teapot(directory=None, width=3840, height=2160, spp=512, env_size=(1024, 512)):
     """C4 of BASELINE.json on the assets SURVEY 8(d) names: the reference's teapot.geo (15,704
-    triangles, UVs) as "plastic" with input/textures/uv.exr (512^2, ZIPS) as rho_d and
-    input/textures/noise.exr (1024^2, ZIPS) as the normal map, on a Lambert plane.geo ground,
-    lit only by an importance-sampled environment light built from a generated 1024x512
+    triangles; the reference reads it without UVs, scene.cpp:183-188) as "plastic" with
+    input/textures/uv.exr (512^2, ZIPS) as rho_d, input/textures/noise.exr (1024^2, ZIPS) as the
+    roughness map and a generated 1024^2 tangent-space normal map (SURVEY's alternative to
+    noise.exr, which is gray noise: as a normal map 32 of its texels give 2t - 1 = 0, a NaN shading
+    frame, and NaN texture coordinates that the reference's (int) texel index turns into an
+    out-of-bounds read -- undefined behaviour, not a parity target), on a Lambert plane.geo
+    ground, lit only by an importance-sampled environment light built from a generated 1024x512
     equirect sky (sky_texture: gradient + Gaussian sun, fixed formula, no RNG).  4K / 512 spp."""
     d = directory or tempfile.mkdtemp(prefix="nart_c4_")
     os.makedirs(d, exist_ok=True)
@@ -419,6 +401,8 @@ def c4_teapot(directory=None, width=3840, height=2160, spp=512, env_size=(1024, 
     plane = reference_mesh("plane", d)
     sky = os.path.join(d, "sky.exr")
     write_texture(sky, sky_texture(env_size[0], env_size[1]))
+    bump = os.path.join(d, "bump.exr")
+    write_texture(bump, tangent_normal_map(1024))
     T = lambda p: {"type": "texture", "filePath": p}  # noqa: E731
     scene = {
         "renderSessions": [{"imageWidth": width, "imageHeight": height, "bucketSize": 16, "spp": spp,
@@ -430,7 +414,7 @@ def c4_teapot(directory=None, width=3840, height=2160, spp=512, env_size=(1024, 
              "material": {"type": "lambert", "rho_d": [0.45, 0.42, 0.38]}},
             {"filePath": teapot,
              "material": {"type": "plastic", "rho_d": T(reference_texture("uv")), "rho_s": [1, 1, 1], "eta": 1.5,
-                          "roughness": 0.25, "normal": T(reference_texture("noise"))}},
+                          "roughness": T(reference_texture("noise")), "normal": T(bump)}},
         ],
         "lights": [{"type": "environment", "Le": T(sky), "intensity": 1.5}],
     }
