@@ -50,7 +50,8 @@ CONFIGS = {
                data="synthesized scene (nart_amd/scenes.py cornell)"),
     "c4": dict(scene=lambda d: scenes.c4_teapot(d), w=3840, h=2160, spp=512, stride=211,
                workload="C4 reference teapot.geo (15,704 triangles) as plastic with input/textures/uv.exr rho_d and "
-                        "noise.exr normal map on a lambert plane.geo, generated 1024x512 environment light, "
+                        "noise.exr roughness map + a generated tangent-space normal map on a lambert plane.geo, "
+                        "generated 1024x512 environment light, "
                         "3840x2160 512spp",
                data="reference meshes/textures packed in assets/ + generated sky EXR (nart_amd/scenes.py c4_teapot)"),
     "c4env": dict(scene=lambda d: scenes.environment(d), w=3840, h=2160, spp=512, stride=211,

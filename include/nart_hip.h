@@ -129,11 +129,12 @@ int nart_hip_bvh_info(const nart_scene_blob* scene, nart_bvh_info* out);
    3 = megakernel, traversal quorum on when the launch spans >= 3 rounds of resident waves. */
 int nart_hip_set_variant(nart_ctx* ctx, int variant);
 
-/* Splat kernel (all bit-identical): 3 = four tile pixels per lane (default); 4 = one bucket per
-   block, samples staged through LDS by source-row chunks; 2, 1, 0 = one tile pixel per lane
-   with the compare-only / threshold / direct filter-index arithmetic.  Modes fall back to the
-   next lower one where their preconditions (power-of-two buckets, threshold table, LDS size)
-   do not hold. */
+/* Splat kernel (all bit-identical): 5 = one lane per tile column sweeping the source rows with a
+   register window of 2*ceil(fw)+1 tile rows; 3 = four tile pixels per lane (default); 4 = one
+   bucket per block, samples staged through LDS by source-row chunks; 2, 1, 0 = one tile pixel
+   per lane with the compare-only / threshold / direct filter-index arithmetic.  Modes fall back
+   to a lower one where their preconditions (power-of-two buckets, threshold table, LDS size,
+   ceil(fw) <= 3) do not hold. */
 int nart_hip_set_splat_mode(nart_ctx* ctx, int mode);
 
 #ifdef __cplusplus

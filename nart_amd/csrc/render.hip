@@ -1078,7 +1078,7 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
                                          : 256u;
         const uint32_t nt = (tpx + lblk - 1) / lblk;
         const int lmode = sa.thr ? (sa.invB != 0.f ? 2 : 1) : 0;
-        if (splat_mode >= 4 && nt <= 4 && (size_t)cw * col_bytes <= (size_t)159 * 1024) {
+        if (splat_mode == 4 && nt <= 4 && (size_t)cw * col_bytes <= (size_t)159 * 1024) {
             const size_t lds = (size_t)cw * col_bytes;
             auto launch_lds = [&](auto kern) {
                 hipLaunchKernelGGL(kern, dim3(nbk), dim3(lblk), lds, st, sa, cw);
@@ -1089,6 +1089,12 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
             NART_SPLAT_LDS_CASE(1, 1) NART_SPLAT_LDS_CASE(1, 2) NART_SPLAT_LDS_CASE(1, 3) NART_SPLAT_LDS_CASE(1, 4)
             NART_SPLAT_LDS_CASE(2, 1) NART_SPLAT_LDS_CASE(2, 2) NART_SPLAT_LDS_CASE(2, 3) NART_SPLAT_LDS_CASE(2, 4)
 #undef NART_SPLAT_LDS_CASE
+        } else if (splat_mode == 5 && sa.thr && sa.invB != 0.f && g.filter_bounds >= 1 && g.filter_bounds <= 3) {
+            const uint64_t nl = (uint64_t)nbk * g.tile_size;  // one lane per tile column
+            const dim3 sw((uint32_t)((nl + 255) / 256));
+            if (g.filter_bounds == 1) hipLaunchKernelGGL(k_splat_sweep<1>, sw, dim3(256), 0, st, sa);
+            else if (g.filter_bounds == 2) hipLaunchKernelGGL(k_splat_sweep<2>, sw, dim3(256), 0, st, sa);
+            else hipLaunchKernelGGL(k_splat_sweep<3>, sw, dim3(256), 0, st, sa);
         } else if (sa.thr && sa.invB != 0.f && splat_mode >= 3)
             hipLaunchKernelGGL(k_splat_col4<NART_SPLAT_NP>, dim3((uint32_t)((n4 + 255) / 256)), dim3(256), 0, st, sa);
         else if (sa.thr && sa.invB != 0.f && splat_mode >= 2) hipLaunchKernelGGL(k_splat<2>, sg, dim3(256), splat_lds, st, sa);
@@ -1220,7 +1226,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     *out = nullptr;
     ctx->device = device_id;
     if (const char* v = std::getenv("NART_VARIANT")) ctx->variant = std::max(0, std::min(3, std::atoi(v)));
-    if (const char* v = std::getenv("NART_SPLAT_MODE")) ctx->splat_mode = std::max(0, std::min(4, std::atoi(v)));
+    if (const char* v = std::getenv("NART_SPLAT_MODE")) ctx->splat_mode = std::max(0, std::min(5, std::atoi(v)));
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device_id || device_id < 0) {
         delete ctx;
@@ -1451,9 +1457,9 @@ int nart_hip_set_splat_mode(nart_ctx* ctx, int mode) {
     if (!ctx) return NART_E_INVALID;
     for (nart_ctx* c : ctx->subs)
         if (int rc = nart_hip_set_splat_mode(c, mode)) return fail(ctx, rc, c->err);
-    if (mode < 0 || mode > 4)
-        return fail(ctx, NART_E_UNSUPPORTED, "splat mode must be 0-4 (4 LDS-staged, 3 four pixels per lane, 2-0 one "
-                                             "pixel per lane)");
+    if (mode < 0 || mode > 5)
+        return fail(ctx, NART_E_UNSUPPORTED, "splat mode must be 0-5 (5 tile-column sweep, 4 LDS-staged, 3 four pixels "
+                                             "per lane, 2-0 one pixel per lane)");
     ctx->splat_mode = mode;
     return NART_OK;
 }

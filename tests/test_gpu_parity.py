@@ -343,7 +343,7 @@ def test_latin_square_high_spp_frame(gpu, glass_scene, glass_oracle):
 
 
 @pytest.mark.parametrize("bucket,fw", [(12, 2.0), (16, 1.0), (8, 2.5), (10, 0.75), (16, 3.0), (4, 0.25)])
-@pytest.mark.parametrize("splat_mode", [4, 3, 0], ids=["lds", "col4", "direct"])
+@pytest.mark.parametrize("splat_mode", [5, 4, 3, 0], ids=["sweep", "lds", "col4", "direct"])
 def test_splat_bucket_and_filter_sizes(gpu, glass_scene, glass_oracle, bucket, fw, splat_mode):
     """Splat arithmetic paths: power-of-two buckets use the compare-only pair test, other sizes
     the direct one; filter widths with threshold-derived indices (fw > ~0.28) and without (0.25);
