@@ -123,18 +123,17 @@ int nart_hip_bvh_info(const nart_scene_blob* scene, nart_bvh_info* out);
 
 /* Kernel variant (all render bit-identical images):
    0 = megakernel with a wave ray queue (default; one lane per pixel slot, the lanes of a wave
-       trace each other's queued shadow and continuation rays),
-   1 = wavefront (ray queues in HBM),
+       trace each other's queued shadow and continuation rays; scenes whose BVH stack does not fit
+       its 512-lane LDS layout run variant 3's kernel),
    2 = megakernel with the traversal quorum on for every launch (parity tests at small sizes),
-   3 = megakernel, traversal quorum on when the launch spans >= 3 rounds of resident waves. */
+   3 = megakernel, traversal quorum on when the launch spans >= 3 rounds of resident waves.
+   1 (the wavefront variant, 2x slower) was retired: NART_E_UNSUPPORTED. */
 int nart_hip_set_variant(nart_ctx* ctx, int variant);
 
-/* Splat kernel (all bit-identical): 5 = one lane per tile column sweeping the source rows with a
-   register window of 2*ceil(fw)+1 tile rows; 3 = four tile pixels per lane (default); 4 = one
-   bucket per block, samples staged through LDS by source-row chunks; 2, 1, 0 = one tile pixel
-   per lane with the compare-only / threshold / direct filter-index arithmetic.  Modes fall back
-   to a lower one where their preconditions (power-of-two buckets, threshold table, LDS size,
-   ceil(fw) <= 3) do not hold. */
+/* Splat kernel (all bit-identical): 3 = four tile pixels per lane (default); 2, 1, 0 = one tile
+   pixel per lane with the compare-only / threshold / direct filter-index arithmetic.  Modes fall
+   back to a lower one where their preconditions (power-of-two buckets, threshold table) do not
+   hold.  (An LDS-staged mode and a tile-column sweep measured slower and were retired.) */
 int nart_hip_set_splat_mode(nart_ctx* ctx, int mode);
 
 #ifdef __cplusplus

@@ -329,13 +329,14 @@ class HipRenderer:
             self.set_splat_mode(splat_mode)
 
     def set_variant(self, variant):
-        """0 = megakernel with a wave ray queue (default), 1 = wavefront (trace/shade over ray
-        queues), 2 / 3 = megakernel with the traversal quorum always / by rounds; identical results."""
+        """0 = megakernel with a wave ray queue (default), 2 / 3 = megakernel with the traversal
+        quorum always / by rounds of resident waves; identical results (1, the wavefront variant,
+        was retired)."""
         self._check(self._lib.nart_hip_set_variant(self._ctx, int(variant)))
 
     def set_splat_mode(self, mode):
-        """3 = four pixels per lane (default), 4 = LDS-staged bucket splat, 2-0 = one pixel per
-        lane (include/nart_hip.h); identical results."""
+        """3 = four tile pixels per lane (default), 2-0 = one pixel per lane (include/nart_hip.h);
+        identical results."""
         self._check(self._lib.nart_hip_set_splat_mode(self._ctx, int(mode)))
 
     def _check(self, rc):

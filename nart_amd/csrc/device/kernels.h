@@ -174,67 +174,6 @@ __global__ __launch_bounds__(256) void k_latin(RenderArgs A) {
     const_cast<uint32_t*>(A.rng0)[slot] = rng;
 }
 
-// K consecutive LatinSquare swaps (sampling.cpp:80-85: swap(a[i], a[c_i]), i = i0 .. i0+K-1) on a
-// lane's index array a[stride 64] in LDS.  The swaps of one lane form a chain of dependent LDS
-// read-modify-writes (one round trip each, and one wave per CU since the arrays fill the LDS).
-// Here the 2K values involved are read at once, the K swaps are replayed on registers -- w[] holds
-// positions i0..i0+K-1, v[j] position c_j for a c_j outside that window (kept equal across
-// repeated c's) -- and the results are written back in order, so the array ends exactly as after
-// the sequential swaps.  For i0 >= n/2 every c_j <= n-1-i0 < i0 lies below the window (no window
-// lookups).
-#ifndef NART_LATIN_K
-#define NART_LATIN_K 8
-#endif
-template <int K, typename T>
-ND void latin_swap_batch(T* a, uint32_t i0, const uint32_t (&c)[K], uint32_t n) {
-    T w[K], v[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-        w[j] = a[(i0 + j) * 64];
-        v[j] = a[c[j] * 64];
-    }
-    if (n - 1u - i0 < i0) {  // wave-uniform: every c_j below the window
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const T vp = w[j];
-            w[j] = v[j];
-#pragma unroll
-            for (int k = j + 1; k < K; ++k)
-                if (c[k] == c[j]) v[k] = vp;
-            v[j] = vp;
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const uint32_t q = c[j], qo = q - i0;
-            const bool inw = qo < (uint32_t)K;
-            T vq = v[j];
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-                if (inw && qo == (uint32_t)k) vq = w[k];
-            const T vp = w[j];
-            w[j] = vq;
-            if (inw) {
-#pragma unroll
-                for (int k = 0; k < K; ++k)
-                    if (qo == (uint32_t)k) w[k] = vp;
-            } else {
-#pragma unroll
-                for (int k = j + 1; k < K; ++k)
-                    if (c[k] == q) v[k] = vp;
-                v[j] = vp;
-            }
-        }
-    }
-    // write back: the window, then the outside positions in batch order (for a repeated c the last
-    // write carries the final value)
-#pragma unroll
-    for (int j = 0; j < K; ++j) a[(i0 + j) * 64] = w[j];
-#pragma unroll
-    for (int j = 0; j < K; ++j)
-        if (c[j] - i0 >= (uint32_t)K) a[c[j] * 64] = v[j];
-}
-
 // Same computation with the two sample arrays in LDS ([spp][64 lanes], bank = lane, so the
 // random-index swaps are conflict-free); one wave per block, spp <= 256 (128 KiB of LDS).
 __global__ __launch_bounds__(64) void k_latin_lds(RenderArgs A) {
@@ -253,20 +192,7 @@ __global__ __launch_bounds__(64) void k_latin_lds(RenderArgs A) {
         xs[i * 64] = ((float)i + rng_float(rng)) * inv;
         ys[i * 64] = ((float)i + rng_float(rng)) * inv;
     }
-    uint32_t i0 = 0;
-#if NART_LATIN_K > 1
-    for (; i0 + NART_LATIN_K <= n; i0 += NART_LATIN_K) {  // batched swaps (latin_swap_batch)
-        uint32_t cx[NART_LATIN_K], cy[NART_LATIN_K];
-#pragma unroll
-        for (int j = 0; j < NART_LATIN_K; ++j) {
-            cx[j] = rng_int(rng, n - 1 - (i0 + j));
-            cy[j] = rng_int(rng, n - 1 - (i0 + j));
-        }
-        latin_swap_batch<NART_LATIN_K, float>(xs, i0, cx, n);
-        latin_swap_batch<NART_LATIN_K, float>(ys, i0, cy, n);
-    }
-#endif
-    for (uint32_t i = i0; i < n; ++i) {
+    for (uint32_t i = 0; i < n; ++i) {
         uint32_t c = rng_int(rng, n - 1 - i);
         float t = xs[i * 64];
         xs[i * 64] = xs[c * 64];
@@ -318,21 +244,7 @@ __global__ __launch_bounds__(64) void k_latin_idx(RenderArgs A, float* scratch) 
             if (dx) ix[i * 64] = (uint16_t)i;
             if (dy) jy[i * 64] = (uint16_t)i;
         }
-        uint32_t i0 = 0;
-#if NART_LATIN_K > 1
-        // batches of K swaps: 2K independent LDS reads, the swaps replayed on registers, 2K writes
-        for (; i0 + NART_LATIN_K <= n; i0 += NART_LATIN_K) {
-            uint32_t cx[NART_LATIN_K], cy[NART_LATIN_K];
-#pragma unroll
-            for (int j = 0; j < NART_LATIN_K; ++j) {
-                cx[j] = rng_int(rng, n - 1 - (i0 + j));  // x choice then y choice, as below
-                cy[j] = rng_int(rng, n - 1 - (i0 + j));
-            }
-            if (dx) latin_swap_batch<NART_LATIN_K, uint16_t>(ix, i0, cx, n);
-            if (dy) latin_swap_batch<NART_LATIN_K, uint16_t>(jy, i0, cy, n);
-        }
-#endif
-        for (uint32_t i = i0; i < n; ++i) {
+        for (uint32_t i = 0; i < n; ++i) {
             uint32_t c = rng_int(rng, n - 1 - i);
             if (dx) {
                 const uint16_t t = ix[i * 64];
@@ -1883,298 +1795,6 @@ __global__ __launch_bounds__(256) void k_splat_col4(SplatArgs A) {
         float* o = A.tiles + ((uint64_t)bi * tpx + (ty0 + j) * A.tile + tx) * 5;
 #pragma unroll
         for (int k = 0; k < 5; ++k) o[k] = c[j][k];
-    }
-}
-
-// One lane per tile COLUMN (tile = B + 2R pixels, R = filterBounds = ceil(fw)), sweeping the
-// bucket's source rows top to bottom.  Source row sy can only reach tile rows sy .. sy + 2R (plus,
-// on a full-height bucket's last row, the bucket-edge wrap rows 0 .. 2R+1, see splat_hits), so the
-// lane keeps those 2R+1 rows' accumulators in registers (win[d] = tile row sy + d): each sample it
-// loads serves 2R+1 tile pixels of its column (col4: 4 of 8 candidate rows), and a bucket's data
-// is fetched ~5.3x per frame instead of ~12.5x (20 tile columns x 16 rows x ~4.25 candidate
-// columns per 256 source pixels).  When sy is done, tile row sy has every normal contribution:
-// it is written out and the window shifts.  The wrap rows get their last contributions (source
-// row bh-1, after all their normal rows) from accumulators reloaded from the tile.  Per tile
-// pixel the order is the reference's: source rows ascending, candidate columns ascending (then
-// the wrap column), samples ascending -- bit-identical to k_splat / k_splat_col4.
-template <int R>
-__global__ __launch_bounds__(256) void k_splat_sweep(SplatArgs A) {
-    __shared__ float s_table[64];
-    __shared__ float s_thr[65];
-    if (threadIdx.x < 64) s_table[threadIdx.x] = A.table[threadIdx.x];
-    if (threadIdx.x < 65) s_thr[threadIdx.x] = A.thr[threadIdx.x];
-    __syncthreads();
-    constexpr int WR = 2 * R + 1;      // window rows
-    constexpr int NWRAP = 2 * R + 2;   // tile rows 0 .. fb + r + 1 that a bucket-edge sample can reach
-    const uint32_t tile = A.tile, tpx = tile * tile;
-    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= (uint64_t)A.n_buckets * tile) return;
-    const uint32_t bi = (uint32_t)(gid / tile), tx = (uint32_t)(gid % tile);
-    const uint32_t bid = A.bucket_ids[bi];
-    const uint32_t bx = bid % A.nbx, by = bid / A.nbx;
-    const uint32_t x0 = A.B * bx, y0 = A.B * by;
-    const uint32_t x1 = min(A.B * (bx + 1), A.totalW), y1 = min(A.B * (by + 1), A.totalH);
-    const int bw = (int)(x1 - x0), bh = (int)(y1 - y0);
-    const uint32_t npx = (uint32_t)(bw * bh);
-    const uint32_t base = A.bucket_base[bi];
-    const int sxlo = max(0, (int)tx - 2 * R), sxhi = min(bw - 1, (int)tx);  // fb == r
-    const bool wrapx = bw == (int)A.B && (int)tx <= 2 * R + 1 && bw - 1 > sxhi;
-    const int ncol = (sxhi >= sxlo ? sxhi - sxlo + 1 : 0) + (wrapx ? 1 : 0);
-    const float fw = A.fw;
-    const float xsA = (float)(tx + x0), xsB = (float)(tx + x0 + A.B);
-    const float edgeX = (float)(x0 + A.B + A.fb), edgeY = (float)(y0 + A.B + A.fb);
-    float* out = A.tiles + ((uint64_t)bi * tpx + tx) * 5;  // tile row ty at out + ty * tile * 5
-    float win[WR][5];
-#pragma unroll
-    for (int d = 0; d < WR; ++d)
-#pragma unroll
-        for (int k = 0; k < 5; ++k) win[d][k] = 0.f;
-    float wra[NWRAP][5];
-#pragma unroll
-    for (int t = 0; t < NWRAP; ++t)
-#pragma unroll
-        for (int k = 0; k < 5; ++k) wra[t][k] = 0.f;
-    auto add_px = [&](float (&c)[5], float ys, float dx2, bool xhit, float scy, float loy, float hiy, float4 L) {
-        const bool hit = xhit && loy < ys + 1.f && ys < hiy;
-        const float distY = (ys + 0.5f) - scy;
-        const float d2 = dx2 + distY * distY;
-        int g = (int)(__builtin_amdgcn_sqrtf(d2) * A.idx_scale);
-        g = g < 0 ? 0 : (g > 63 ? 63 : g);
-        const float t0 = s_thr[g], t1 = s_thr[g + 1];
-        const int fi = g - (d2 < t0 ? 1 : 0) + (d2 >= t1 ? 1 : 0);
-        const float w = s_table[fi];
-        if (hit) {
-            c[0] += L.x * w;
-            c[1] += L.y * w;
-            c[2] += L.z * w;
-            c[3] += L.w * w;
-            c[4] += w;
-        }
-    };
-    for (int sy = 0; sy < bh; ++sy) {
-        // the wrap rows take part in the bucket's last source row (full-height buckets only)
-        const bool wrap_row = sy == bh - 1 && bh == (int)A.B;
-        if (wrap_row) {
-#pragma unroll
-            for (int t = 0; t < NWRAP; ++t)
-                if (t < sy)  // rows already written out (all of them for B > 2R + 2)
-#pragma unroll
-                    for (int k = 0; k < 5; ++k) wra[t][k] = out[(size_t)t * tile * 5 + k];
-        }
-        const float fy = (float)(y0 + (uint32_t)sy + A.fb);
-        const float ysA = (float)(y0 + (uint32_t)sy), ysB = ysA + (float)A.B;  // tile row sy + d -> ys + d
-        const float ywA = (float)y0, ywB = (float)(y0 + A.B);                  // wrap row t -> yw + t
-        for (int ci = 0; ci < ncol; ++ci) {
-            const int sx = (sxlo + ci <= sxhi) ? sxlo + ci : bw - 1;
-            const float fx = (float)(x0 + (uint32_t)sx + A.fb);
-            const uint64_t first = (uint64_t)base * A.spp + (uint32_t)(sy * bw + sx);
-            const float2* sp = A.samples + first;
-            const float4* lp = A.Lout + first;
-            auto splat1 = [&](float2 uv, float4 L) {
-                const float scx = fx + uv.x, scy = fy + uv.y;
-                const float xs = scx >= edgeX ? xsB : xsA;
-                const bool xhit = (scx - fw) < xs + 1.f && xs < (scx + fw);
-                const float distX = (xs + 0.5f) - scx;
-                const float dx2 = distX * distX;
-                const bool yedge = scy >= edgeY;
-                const float loy = scy - fw, hiy = scy + fw;
-                const float yb = yedge ? ysB : ysA;
-#pragma unroll
-                for (int d = 0; d < WR; ++d) add_px(win[d], yb + (float)d, dx2, xhit, scy, loy, hiy, L);
-                if (wrap_row) {
-                    const float wb = yedge ? ywB : ywA;
-#pragma unroll
-                    for (int t = 0; t < NWRAP; ++t)
-                        if (t < sy) add_px(wra[t], wb + (float)t, dx2, xhit, scy, loy, hiy, L);
-                }
-            };
-            constexpr uint32_t PF = 4;  // samples per group; the next group is in flight
-            uint32_t i = 0;
-            float2 nu[PF];
-            float4 nL[PF];
-            if (A.spp >= PF) {
-#pragma unroll
-                for (uint32_t u = 0; u < PF; ++u) {
-                    nu[u] = sp[(size_t)u * npx];
-                    nL[u] = lp[(size_t)u * npx];
-                }
-            }
-            for (; i + PF <= A.spp; i += PF) {
-                float2 uv[PF];
-                float4 Lv[PF];
-#pragma unroll
-                for (uint32_t u = 0; u < PF; ++u) {
-                    uv[u] = nu[u];
-                    Lv[u] = nL[u];
-                }
-                if (i + 2 * PF <= A.spp) {
-                    const size_t k0 = (size_t)(i + PF) * npx;
-#pragma unroll
-                    for (uint32_t u = 0; u < PF; ++u) {
-                        nu[u] = sp[k0 + (size_t)u * npx];
-                        nL[u] = lp[k0 + (size_t)u * npx];
-                    }
-                }
-#pragma unroll
-                for (uint32_t u = 0; u < PF; ++u) splat1(uv[u], Lv[u]);
-            }
-            for (; i < A.spp; ++i) splat1(sp[(size_t)i * npx], lp[(size_t)i * npx]);
-        }
-        if (wrap_row) {
-#pragma unroll
-            for (int t = 0; t < NWRAP; ++t)
-                if (t < sy)
-#pragma unroll
-                    for (int k = 0; k < 5; ++k) out[(size_t)t * tile * 5 + k] = wra[t][k];
-        }
-        // tile row sy is complete (the wrap rows were reloaded above): write it, shift the window
-#pragma unroll
-        for (int k = 0; k < 5; ++k) out[(size_t)sy * tile * 5 + k] = win[0][k];
-#pragma unroll
-        for (int d = 0; d + 1 < WR; ++d)
-#pragma unroll
-            for (int k = 0; k < 5; ++k) win[d][k] = win[d + 1][k];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) win[WR - 1][k] = 0.f;
-    }
-    // rows bh .. bh + 2R - 1 are in the window; rows beyond were never reached
-    for (int ty = bh; ty < (int)tile; ++ty) {
-        const int d = ty - bh;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            float v = 0.f;
-#pragma unroll
-            for (int e = 0; e + 1 < WR; ++e)
-                if (d == e) v = win[e][k];
-            out[(size_t)ty * tile * 5 + k] = v;
-        }
-    }
-}
-
-// Splat with one bucket per block and the bucket's samples staged through LDS once.
-// A tile pixel receives its samples in (source pixel raster, sample) order, so the bucket is
-// swept source row by source row (and, when a whole row does not fit, in ascending column
-// chunks): each chunk's samples and radiance are read from HBM once into LDS ([sample][column]),
-// then every tile pixel whose candidate rows include this row adds the chunk's candidate columns
-// in ascending order.  The per-pair arithmetic is k_splat's (MODE as there), so tiles are
-// bit-identical.  (k_splat_col4 instead re-reads each bucket's ~1.5 MB through an L2 that the
-// many buckets in flight per XCD keep missing: 80 GB of fetches for 12.8 GB of data at C3.)
-// NT tile pixels per lane (tile^2 <= NT * blockDim); cw: columns per staged chunk.
-template <int MODE, int NT>
-__global__ __launch_bounds__(256) void k_splat_lds(SplatArgs A, uint32_t cw) {
-    extern __shared__ __attribute__((aligned(16))) float4 s_chunk[];  // L [spp][w], then uv [spp][w]
-    __shared__ float s_table[64];
-    __shared__ float s_thr[65];
-    if (threadIdx.x < 64) s_table[threadIdx.x] = A.table[threadIdx.x];
-    if (MODE > 0 && threadIdx.x < 65) s_thr[threadIdx.x] = A.thr[threadIdx.x];
-    const uint32_t bi = blockIdx.x;
-    const uint32_t bid = A.bucket_ids[bi];
-    const uint32_t bx = bid % A.nbx, by = bid / A.nbx;
-    const uint32_t x0 = A.B * bx, y0 = A.B * by;
-    const uint32_t x1 = min(A.B * (bx + 1), A.totalW), y1 = min(A.B * (by + 1), A.totalH);
-    const int bw = (int)(x1 - x0), bh = (int)(y1 - y0);
-    const uint32_t npx = (uint32_t)(bw * bh);
-    const uint32_t base = A.bucket_base[bi];
-    const int r = (int)ceilf(A.fw), fb = (int)A.fb;
-    const uint32_t tpx = A.tile * A.tile;
-    const uint32_t spp = A.spp;
-    float c[NT][5];
-#pragma unroll
-    for (int k = 0; k < NT; ++k)
-#pragma unroll
-        for (int j = 0; j < 5; ++j) c[k][j] = 0.f;
-    for (int sy = 0; sy < bh; ++sy) {
-        const float fy = (float)(y0 + (uint32_t)sy + A.fb);
-        for (int c0 = 0; c0 < bw; c0 += (int)cw) {
-            const int w = min((int)cw, bw - c0);
-            float4* sL = s_chunk;
-            float2* sU = reinterpret_cast<float2*>(s_chunk + (size_t)spp * w);
-            __syncthreads();
-            {
-                const uint64_t row0 = (uint64_t)base * spp + (uint32_t)(sy * bw + c0);
-                for (uint32_t i = threadIdx.x; i < spp * (uint32_t)w; i += blockDim.x) {
-                    const uint32_t s = i / (uint32_t)w, col = i - s * (uint32_t)w;
-                    const uint64_t idx = row0 + (uint64_t)s * npx + col;
-                    sL[i] = A.Lout[idx];
-                    sU[i] = A.samples[idx];
-                }
-            }
-            __syncthreads();
-#pragma unroll
-            for (int k = 0; k < NT; ++k) {
-                const uint32_t t = threadIdx.x + (uint32_t)k * blockDim.x;
-                if (t >= tpx) continue;
-                const int tx = (int)(t % A.tile), ty = (int)(t / A.tile);
-                const int sylo = max(0, ty - fb - r), syhi = min(bh - 1, ty - fb + r);
-                const bool wrapy = bh == (int)A.B && ty <= fb + r + 1 && bh - 1 > syhi;
-                if (!((sy >= sylo && sy <= syhi) || (wrapy && sy == bh - 1))) continue;
-                const int sxlo = max(0, tx - fb - r), sxhi = min(bw - 1, tx - fb + r);
-                const bool wrapx = bw == (int)A.B && tx <= fb + r + 1 && bw - 1 > sxhi;
-                SplatLane P;
-                P.xsA = (float)((uint32_t)tx + x0);
-                P.xsB = (float)((uint32_t)tx + x0 + A.B);
-                P.ysA = (float)((uint32_t)ty + y0);
-                P.ysB = (float)((uint32_t)ty + y0 + A.B);
-                P.edgeX = (float)(x0 + A.B + A.fb);
-                P.edgeY = (float)(y0 + A.B + A.fb);
-                const uint32_t utx = (uint32_t)tx, uty = (uint32_t)ty;
-                (void)utx;
-                (void)uty;
-                // candidate columns of this chunk in ascending order, then the bucket-edge wrap column
-                const int lo = max(sxlo, c0), hi = min(sxhi, c0 + w - 1);
-                const int ncol = (hi >= lo ? hi - lo + 1 : 0) + ((wrapx && bw - 1 >= c0 && bw - 1 < c0 + w) ? 1 : 0);
-                for (int ci = 0; ci < ncol; ++ci) {
-                    const int sx = (lo + ci <= hi) ? lo + ci : bw - 1;
-                    const float fx = (float)(x0 + (uint32_t)sx + A.fb);
-                    const float4* lp = sL + (sx - c0);
-                    const float2* up = sU + (sx - c0);
-                    auto hit1 = [&](float2 uv, float& wt) {
-                        return MODE == 2 ? splat_hits_fast(A, P, s_table, s_thr, fx + uv.x, fy + uv.y, wt)
-                             : MODE == 1 ? splat_hits_thr(A, s_table, s_thr, fx + uv.x, fy + uv.y, utx, uty, wt)
-                                         : splat_hits(A, s_table, fx + uv.x, fy + uv.y, utx, uty, wt);
-                    };
-                    auto add1 = [&](bool h, float wt, float4 Lv) {
-                        if (h) {
-                            c[k][0] += Lv.x * wt;
-                            c[k][1] += Lv.y * wt;
-                            c[k][2] += Lv.z * wt;
-                            c[k][3] += Lv.w * wt;
-                            c[k][4] += wt;
-                        }
-                    };
-                    // groups of 4 samples: loads and pair tests independent, sums in sample order
-                    uint32_t s = 0;
-                    for (; s + 4 <= spp; s += 4) {
-                        float2 uv[4];
-                        float4 Lv[4];
-                        float wt[4];
-                        bool h[4];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            uv[u] = up[(size_t)(s + u) * w];
-                            Lv[u] = lp[(size_t)(s + u) * w];
-                        }
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) h[u] = hit1(uv[u], wt[u]);
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) add1(h[u], wt[u], Lv[u]);
-                    }
-                    for (; s < spp; ++s) {
-                        float wt;
-                        const bool h = hit1(up[(size_t)s * w], wt);
-                        add1(h, wt, lp[(size_t)s * w]);
-                    }
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < NT; ++k) {
-        const uint32_t t = threadIdx.x + (uint32_t)k * blockDim.x;
-        if (t >= tpx) continue;
-        float* o = A.tiles + ((uint64_t)bi * tpx + t) * 5;
-#pragma unroll
-        for (int j = 0; j < 5; ++j) o[j] = c[k][j];
     }
 }
 

@@ -17,7 +17,6 @@
 
 #include "../../include/nart_hip.h"
 #include "device/volume.h"
-#include "device/wavefront.h"
 #include "host/bvh_build.h"
 
 using namespace nd;
@@ -29,7 +28,7 @@ struct nart_ctx {
     uint32_t stack_depth = 1;
     uint32_t num_nodes = 0;
     int variant = 0;
-    // 3 four pixels per lane (default), 4 LDS-staged (C3: 117 vs 33 ms), 2/1/0 one pixel per lane
+    // 3 four pixels per lane (default), 2/1/0 one pixel per lane
     int splat_mode = 3;
     bool counters = false;
     bool has_env = false;  // scene has an environment light (selects the k_render build)
@@ -69,14 +68,6 @@ struct nart_ctx {
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // ev[4]: after k_primary
     bool primary_ran = false;  // the last dispatch launched k_primary (ev[4] recorded)
     bool events = false;
-    // wavefront variant: path state + queues (one allocation), pinned queue-count readback
-    void* d_wf = nullptr;
-    size_t cap_wf = 0;
-    uint32_t* h_counts = nullptr;
-    hipEvent_t ev_chunk[2] = {nullptr, nullptr};
-    uint32_t wf_grid_trace = 0, wf_grid_shade = 0;
-    uint64_t wf_iterations = 0;
-    uint64_t stat_counts[5] = {0, 0, 0, 0, 0};
     // megakernel work queue (launch_render)
     uint32_t* d_queue = nullptr;
     uint32_t* d_cost = nullptr;
@@ -287,8 +278,20 @@ int check_params(nart_ctx* ctx, const nart_render_params* p) {
     return NART_OK;
 }
 
-size_t batch_slot_limit(uint32_t spp) {
+// Per-sample state of one batch (LatinSquare sample, radiance, camera hit: 28 B per sample).  An
+// MI355X holds 288 GB, so by default a batch may take half of the device memory free at the call
+// (plus what this context already holds for it), at least 16 GiB: whole frames up to 4K x 512 spp
+// (119 GB) render in one batch -- fewer launch tails than the former fixed 16 GiB (C5 469 -> 413
+// ms, C4 5.27 -> 4.43 s per frame; profiles/r03a_batch_ab.log).  NART_BATCH_BYTES overrides.
+size_t batch_slot_limit(const nart_ctx* ctx, uint32_t spp) {
     size_t budget = (size_t)16 << 30;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+        const size_t held = ctx->cap_samples * (sizeof(float2) + sizeof(float4) + sizeof(uint32_t));
+        budget = std::max(budget, (free_b + held) / 2);
+    } else {
+        (void)hipGetLastError();
+    }
     if (const char* e = std::getenv("NART_BATCH_BYTES")) budget = (size_t)std::strtoull(e, nullptr, 10);
     size_t per = 8 + (size_t)spp * (sizeof(float2) + sizeof(float4) + sizeof(uint32_t));
     size_t n = budget / per;
@@ -726,114 +729,6 @@ int dispatch_megakernel(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     return ctx->has_env ? launch_render_maxl<true>(ctx, a, st) : launch_render_maxl<false>(ctx, a, st);
 }
 
-// ---------------------------------------------------------------- wavefront variant
-// Carve the path state and queues for n slots out of one allocation (256-B aligned rows).
-int wf_layout(nart_ctx* ctx, uint32_t n, int maxl, WFArgs& w) {
-    size_t off = 0;
-    auto take = [&](size_t bytes) {
-        size_t o = off;
-        off += (bytes + 255) & ~(size_t)255;
-        return o;
-    };
-    const size_t N = n;
-    size_t o_u = take(N * 16), o_L = take(N * 16), o_beta = take(N * 16), o_misc = take(N * 16);
-    size_t o_c1 = take(N * 16), o_c2 = take(N * 16), o_bk = take(N * 16);
-    size_t o_ro = take(3 * N * 16), o_rd = take(3 * N * 16), o_hit = take(N * 8), o_occ = take(3 * N);
-    size_t o_ln = take(N * 4), o_lid = take((size_t)maxl * N * 4), o_leta = take((size_t)maxl * N * 4);
-    size_t o_re0 = take(N * 4), o_re1 = take(N * 4), o_rs0 = take(2 * N * 4), o_rs1 = take(2 * N * 4);
-    size_t o_cnt = take(6 * 4);
-    if (off > ctx->cap_wf) {
-        if (ctx->d_wf) hipFree(ctx->d_wf);
-        ctx->d_wf = nullptr;
-        ctx->cap_wf = 0;
-        if (int rc = dmalloc(ctx, &ctx->d_wf, off, "wavefront state")) return rc;
-        ctx->cap_wf = off;
-    }
-    char* b = static_cast<char*>(ctx->d_wf);
-    WFState& T = w.st;
-    T.u = (uint4*)(b + o_u);
-    T.L = (float4*)(b + o_L);
-    T.beta = (float4*)(b + o_beta);
-    T.misc = (float4*)(b + o_misc);
-    T.c1 = (float4*)(b + o_c1);
-    T.c2 = (float4*)(b + o_c2);
-    T.betak = (float4*)(b + o_bk);
-    T.ray_o = (float4*)(b + o_ro);
-    T.ray_d = (float4*)(b + o_rd);
-    T.hit = (uint2*)(b + o_hit);
-    T.occ = (uint8_t*)(b + o_occ);
-    T.ln = (uint32_t*)(b + o_ln);
-    T.lid = (uint32_t*)(b + o_lid);
-    T.leta = (float*)(b + o_leta);
-    w.rq_ext[0] = (uint32_t*)(b + o_re0);
-    w.rq_ext[1] = (uint32_t*)(b + o_re1);
-    w.rq_sh[0] = (uint32_t*)(b + o_rs0);
-    w.rq_sh[1] = (uint32_t*)(b + o_rs1);
-    w.counts = (uint32_t*)(b + o_cnt);
-    return NART_OK;
-}
-
-// Persistent grids: as many resident blocks as the occupancy calculator allows on every CU.
-template <int MAXL, bool COUNT>
-int wf_grids(nart_ctx* ctx, size_t lds) {
-    int cus = 0, bt = 0, bs = 0;
-    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bt, (const void*)k_wf_trace<COUNT>, 256, lds));
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bs, (const void*)k_wf_shade<MAXL>, 256, 0));
-    ctx->wf_grid_trace = (uint32_t)std::max(1, cus * std::max(bt, 1));
-    ctx->wf_grid_shade = (uint32_t)std::max(1, cus * std::max(bs, 1));
-    return NART_OK;
-}
-
-// Iterate trace/shade until every slot has retired.  Queue counts are read back in chunks of
-// iterations, one chunk behind the launches, so the GPU never waits for the host.
-template <int MAXL, bool COUNT>
-int run_wavefront(nart_ctx* ctx, const RenderArgs& ra, hipStream_t st) {
-    WFArgs w;
-    w.R = ra;
-    int rc = wf_layout(ctx, ra.n_slots, MAXL, w);
-    if (rc) return rc;
-    const size_t lds = (size_t)ctx->stack_depth * 256 * 8;
-    if ((rc = wf_grids<MAXL, COUNT>(ctx, lds))) return rc;
-    if (!ctx->h_counts) {
-        HIPCHK(hipHostMalloc((void**)&ctx->h_counts, 4 * sizeof(uint32_t), hipHostMallocDefault));
-        for (auto& e : ctx->ev_chunk) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    }
-    HIPCHK(hipMemsetAsync(w.counts, 0, 6 * sizeof(uint32_t), st));
-    const uint32_t init_grid = std::min<uint32_t>((ra.n_slots + 255) / 256, 4096);
-    hipLaunchKernelGGL(k_wf_init, dim3(init_grid), dim3(256), 0, st, ctx->scene, w);
-    HIPCHK(hipGetLastError());
-    if (ra.bounces == 0) return NART_OK;
-    // every shade advances each live slot by one bounce or one sample, plus one final resolve
-    const uint64_t max_it = (uint64_t)ra.spp * (ra.bounces + 1) + 2;
-    const uint32_t K = 8;
-    uint32_t it = 0;
-    for (uint32_t chunk = 0;; ++chunk) {
-        for (uint32_t j = 0; j < K; ++j, ++it) {
-            hipLaunchKernelGGL((k_wf_trace<COUNT>), dim3(ctx->wf_grid_trace), dim3(256), lds, st, ctx->scene, w, it);
-            hipLaunchKernelGGL((k_wf_shade<MAXL>), dim3(ctx->wf_grid_shade), dim3(256), 0, st, ctx->scene, w, it);
-        }
-        HIPCHK(hipGetLastError());
-        // slots queued for iteration `it` (written by shade(it - 1))
-        HIPCHK(hipMemcpyAsync(&ctx->h_counts[chunk & 1], &w.counts[4 + (it & 1)], 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipEventRecord(ctx->ev_chunk[chunk & 1], st));
-        if (chunk > 0) {
-            HIPCHK(hipEventSynchronize(ctx->ev_chunk[(chunk - 1) & 1]));
-            if (ctx->h_counts[(chunk - 1) & 1] == 0) break;
-        }
-        if (it > max_it + 2 * K) return fail(ctx, NART_E_HIP, "wavefront queues did not drain");
-    }
-    ctx->wf_iterations += it;
-    return NART_OK;
-}
-
-int dispatch_wavefront(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
-    const bool c = ctx->counters;
-    if (a.bounces <= 10) return c ? run_wavefront<10, true>(ctx, a, st) : run_wavefront<10, false>(ctx, a, st);
-    if (a.bounces <= 16) return c ? run_wavefront<16, true>(ctx, a, st) : run_wavefront<16, false>(ctx, a, st);
-    return c ? run_wavefront<32, true>(ctx, a, st) : run_wavefront<32, false>(ctx, a, st);
-}
-
 // Volume integrator: k_render_volume_sm (lanes advance one tentative collision per iteration and
 // start their next sample independently).  When the shard spans several rounds of resident
 // waves, the costliest wave-sized pixel groups (cost probe: tentative collisions of 4 samples per
@@ -881,7 +776,7 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
 
 int dispatch_render(nart_ctx* ctx, const RenderArgs& a, int integrator, hipStream_t st) {
     if (integrator == NART_INTEGRATOR_VOLUME) return dispatch_volume(ctx, a, st);
-    return ctx->variant == 1 ? dispatch_wavefront(ctx, a, st) : dispatch_megakernel(ctx, a, st);
+    return dispatch_megakernel(ctx, a, st);
 }
 
 // Filter index of AddSample (render.cpp:43-49) as a function of d2 = distX^2 + distY^2:
@@ -972,7 +867,7 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         for (auto& e : ctx->ev) HIPCHK(hipEventCreate(&e));
         ctx->events = true;
     }
-    const size_t limit = batch_slot_limit(p->spp);
+    const size_t limit = batch_slot_limit(ctx, p->spp);
     const uint32_t tpx = g.tile_size * g.tile_size;
     double kernel_ms = 0.0, splat_ms = 0.0, latin_ms = 0.0, primary_ms = 0.0;
     uint32_t launches = 0;
@@ -1058,48 +953,19 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
             sa.invFw = (m == 0.5f) ? 1.f / p->filter_width : 0.f;
         }
         uint64_t nthreads = (uint64_t)nbk * tpx;
-        static const size_t splat_lds =
-            std::getenv("NART_SPLAT_LDS") ? std::strtoull(std::getenv("NART_SPLAT_LDS"), nullptr, 10) : 0;
         const int splat_mode = ctx->splat_mode;
         const dim3 sg((uint32_t)((nthreads + 255) / 256));
 #ifndef NART_SPLAT_NP
 #define NART_SPLAT_NP 4
 #endif
         const uint64_t n4 = (uint64_t)nbk * g.tile_size * ((g.tile_size + NART_SPLAT_NP - 1) / NART_SPLAT_NP);
-        // mode 4 (selectable; mode 3 is the default): bucket per block, samples staged through LDS
-        // in source-row chunks of cw columns (NART_SPLAT_CHUNK_KB of LDS per block)
-        static const size_t chunk_kb =
-            std::getenv("NART_SPLAT_CHUNK_KB") ? std::strtoull(std::getenv("NART_SPLAT_CHUNK_KB"), nullptr, 10) : 48;
-        const size_t col_bytes = (size_t)p->spp * (sizeof(float4) + sizeof(float2));
-        const uint32_t cw = (uint32_t)std::min<size_t>(p->bucket_size, std::max<size_t>(1, chunk_kb * 1024 / col_bytes));
-        // k_splat_lds is declared __launch_bounds__(256): larger blocks would not launch
-        static const uint32_t lblk = std::getenv("NART_SPLAT_LDS_BLOCK")
-                                         ? (uint32_t)std::max(64, std::min(256, std::atoi(std::getenv("NART_SPLAT_LDS_BLOCK"))))
-                                         : 256u;
-        const uint32_t nt = (tpx + lblk - 1) / lblk;
-        const int lmode = sa.thr ? (sa.invB != 0.f ? 2 : 1) : 0;
-        if (splat_mode == 4 && nt <= 4 && (size_t)cw * col_bytes <= (size_t)159 * 1024) {
-            const size_t lds = (size_t)cw * col_bytes;
-            auto launch_lds = [&](auto kern) {
-                hipLaunchKernelGGL(kern, dim3(nbk), dim3(lblk), lds, st, sa, cw);
-            };
-#define NART_SPLAT_LDS_CASE(M, N) \
-    if (lmode == M && nt == N) launch_lds(k_splat_lds<M, N>);
-            NART_SPLAT_LDS_CASE(0, 1) NART_SPLAT_LDS_CASE(0, 2) NART_SPLAT_LDS_CASE(0, 3) NART_SPLAT_LDS_CASE(0, 4)
-            NART_SPLAT_LDS_CASE(1, 1) NART_SPLAT_LDS_CASE(1, 2) NART_SPLAT_LDS_CASE(1, 3) NART_SPLAT_LDS_CASE(1, 4)
-            NART_SPLAT_LDS_CASE(2, 1) NART_SPLAT_LDS_CASE(2, 2) NART_SPLAT_LDS_CASE(2, 3) NART_SPLAT_LDS_CASE(2, 4)
-#undef NART_SPLAT_LDS_CASE
-        } else if (splat_mode == 5 && sa.thr && sa.invB != 0.f && g.filter_bounds >= 1 && g.filter_bounds <= 3) {
-            const uint64_t nl = (uint64_t)nbk * g.tile_size;  // one lane per tile column
-            const dim3 sw((uint32_t)((nl + 255) / 256));
-            if (g.filter_bounds == 1) hipLaunchKernelGGL(k_splat_sweep<1>, sw, dim3(256), 0, st, sa);
-            else if (g.filter_bounds == 2) hipLaunchKernelGGL(k_splat_sweep<2>, sw, dim3(256), 0, st, sa);
-            else hipLaunchKernelGGL(k_splat_sweep<3>, sw, dim3(256), 0, st, sa);
-        } else if (sa.thr && sa.invB != 0.f && splat_mode >= 3)
+        // splat modes (all bit-identical, mode 3 the default): 3 four tile pixels per lane; 2 / 1 / 0
+        // one tile pixel per lane with the compare-only / threshold / direct filter-index arithmetic
+        if (sa.thr && sa.invB != 0.f && splat_mode >= 3)
             hipLaunchKernelGGL(k_splat_col4<NART_SPLAT_NP>, dim3((uint32_t)((n4 + 255) / 256)), dim3(256), 0, st, sa);
-        else if (sa.thr && sa.invB != 0.f && splat_mode >= 2) hipLaunchKernelGGL(k_splat<2>, sg, dim3(256), splat_lds, st, sa);
-        else if (sa.thr && splat_mode >= 1) hipLaunchKernelGGL(k_splat<1>, sg, dim3(256), splat_lds, st, sa);
-        else hipLaunchKernelGGL(k_splat<0>, sg, dim3(256), splat_lds, st, sa);
+        else if (sa.thr && sa.invB != 0.f && splat_mode >= 2) hipLaunchKernelGGL(k_splat<2>, sg, dim3(256), 0, st, sa);
+        else if (sa.thr && splat_mode >= 1) hipLaunchKernelGGL(k_splat<1>, sg, dim3(256), 0, st, sa);
+        else hipLaunchKernelGGL(k_splat<0>, sg, dim3(256), 0, st, sa);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(ctx->ev[2], st));
         HIPCHK(hipEventSynchronize(ctx->ev[2]));
@@ -1225,8 +1091,11 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     if (!ctx) return NART_E_OOM;
     *out = nullptr;
     ctx->device = device_id;
-    if (const char* v = std::getenv("NART_VARIANT")) ctx->variant = std::max(0, std::min(3, std::atoi(v)));
-    if (const char* v = std::getenv("NART_SPLAT_MODE")) ctx->splat_mode = std::max(0, std::min(5, std::atoi(v)));
+    if (const char* v = std::getenv("NART_VARIANT")) {
+        const int var = std::atoi(v);
+        if (var == 0 || var == 2 || var == 3) ctx->variant = var;
+    }
+    if (const char* v = std::getenv("NART_SPLAT_MODE")) ctx->splat_mode = std::max(0, std::min(3, std::atoi(v)));
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device_id || device_id < 0) {
         delete ctx;
@@ -1245,15 +1114,6 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     if (hipFuncSetAttribute((const void*)k_latin_idx, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
         hipSuccess)
         return bail(NART_E_HIP);
-    hipFuncSetAttribute((const void*)k_splat<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
-    hipFuncSetAttribute((const void*)k_splat<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
-    hipFuncSetAttribute((const void*)k_splat<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
-    for (const void* f : {(const void*)k_splat_lds<0, 1>, (const void*)k_splat_lds<0, 2>, (const void*)k_splat_lds<0, 3>,
-                          (const void*)k_splat_lds<0, 4>, (const void*)k_splat_lds<1, 1>, (const void*)k_splat_lds<1, 2>,
-                          (const void*)k_splat_lds<1, 3>, (const void*)k_splat_lds<1, 4>, (const void*)k_splat_lds<2, 1>,
-                          (const void*)k_splat_lds<2, 2>, (const void*)k_splat_lds<2, 3>, (const void*)k_splat_lds<2, 4>})
-        hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
-    (void)hipGetLastError();  // the splat LDS limit is a tuning knob (NART_SPLAT_LDS), not required
     // reference octree visibility (Q14) + device BVH
     std::vector<uint8_t> mask;
     bool root_leaf = false;
@@ -1428,7 +1288,7 @@ void nart_hip_destroy(nart_ctx* ctx) {
     hipSetDevice(ctx->device);
     void* bufs[] = {ctx->d_nodes, ctx->d_tri_isect, ctx->d_tri_perm, ctx->d_tris, ctx->d_tri_mesh, ctx->d_meshes, ctx->d_mats,
                     ctx->d_lights, ctx->d_texs, ctx->d_tex_pool, ctx->d_slot_xy, ctx->d_slot_so, ctx->d_rng, ctx->d_samples, ctx->d_prim,
-                    ctx->d_L, ctx->d_bucket_ids, ctx->d_bucket_base, ctx->d_table, ctx->d_counters, ctx->d_wf, ctx->d_envs, ctx->d_density,
+                    ctx->d_L, ctx->d_bucket_ids, ctx->d_bucket_base, ctx->d_table, ctx->d_counters, ctx->d_envs, ctx->d_density,
                     ctx->d_oc_nodes, ctx->d_oc_chunks, ctx->d_oc_tris, ctx->d_tri_leaf, ctx->d_oc_lock, ctx->d_oc_heap,
                     ctx->d_queue, ctx->d_cost, ctx->d_keys[0], ctx->d_keys[1], ctx->d_vals[0], ctx->d_vals[1],
                     ctx->d_qhead, ctx->d_sort_tmp};
@@ -1437,10 +1297,6 @@ void nart_hip_destroy(nart_ctx* ctx) {
     for (void* b : ctx->env_bufs) hipFree(b);
     if (ctx->events)
         for (auto& e : ctx->ev) hipEventDestroy(e);
-    if (ctx->h_counts) {
-        hipHostFree(ctx->h_counts);
-        for (auto& e : ctx->ev_chunk) hipEventDestroy(e);
-    }
     delete ctx;
 }
 
@@ -1457,9 +1313,9 @@ int nart_hip_set_splat_mode(nart_ctx* ctx, int mode) {
     if (!ctx) return NART_E_INVALID;
     for (nart_ctx* c : ctx->subs)
         if (int rc = nart_hip_set_splat_mode(c, mode)) return fail(ctx, rc, c->err);
-    if (mode < 0 || mode > 5)
-        return fail(ctx, NART_E_UNSUPPORTED, "splat mode must be 0-5 (5 tile-column sweep, 4 LDS-staged, 3 four pixels "
-                                             "per lane, 2-0 one pixel per lane)");
+    if (mode < 0 || mode > 3)
+        return fail(ctx, NART_E_UNSUPPORTED, "splat mode must be 0-3 (3 four pixels per lane, 2-0 one pixel per lane; "
+                                             "the LDS-staged and tile-column-sweep modes were retired, DESIGN.md)");
     ctx->splat_mode = mode;
     return NART_OK;
 }
@@ -1468,9 +1324,10 @@ int nart_hip_set_variant(nart_ctx* ctx, int variant) {
     if (!ctx) return NART_E_INVALID;
     for (nart_ctx* c : ctx->subs)
         if (int rc = nart_hip_set_variant(c, variant)) return fail(ctx, rc, c->err);
-    if (variant < 0 || variant > 3)
-        return fail(ctx, NART_E_UNSUPPORTED, "variant must be 0 (megakernel with a wave ray queue), 1 (wavefront), 2 "
-                                             "(megakernel, traversal quorum always) or 3 (megakernel, quorum by rounds)");
+    if (variant < 0 || variant > 3 || variant == 1)
+        return fail(ctx, NART_E_UNSUPPORTED, "variant must be 0 (megakernel with a wave ray queue), 2 (megakernel, "
+                                             "traversal quorum always) or 3 (megakernel, quorum by rounds); the "
+                                             "wavefront variant 1 was retired (2x slower, DESIGN.md)");
     ctx->variant = variant;
     return NART_OK;
 }

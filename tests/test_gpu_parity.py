@@ -31,10 +31,10 @@ def _report(a, b):
     return "%d of %d floats differ, max abs diff %g" % (int(ne.sum()), ne.size, float(np.nanmax(np.abs(a - b))))
 
 
-# ray-queue megakernel (default), wavefront, megakernel with the traversal quorum forced on,
-# megakernel with the quorum chosen by rounds of resident waves
-VARIANTS = [0, 1, 2, 3]
-VARIANT_IDS = ["rayqueue", "wavefront", "quorum", "megakernel"]
+# ray-queue megakernel (default), megakernel with the traversal quorum forced on, megakernel with
+# the quorum chosen by rounds of resident waves (the wavefront variant was retired in round 3)
+VARIANTS = [0, 2, 3]
+VARIANT_IDS = ["rayqueue", "quorum", "megakernel"]
 
 
 @pytest.fixture(scope="module", params=VARIANTS, ids=VARIANT_IDS)
@@ -343,11 +343,11 @@ def test_latin_square_high_spp_frame(gpu, glass_scene, glass_oracle):
 
 
 @pytest.mark.parametrize("bucket,fw", [(12, 2.0), (16, 1.0), (8, 2.5), (10, 0.75), (16, 3.0), (4, 0.25)])
-@pytest.mark.parametrize("splat_mode", [5, 4, 3, 0], ids=["sweep", "lds", "col4", "direct"])
+@pytest.mark.parametrize("splat_mode", [3, 2, 0], ids=["col4", "compare", "direct"])
 def test_splat_bucket_and_filter_sizes(gpu, glass_scene, glass_oracle, bucket, fw, splat_mode):
     """Splat arithmetic paths: power-of-two buckets use the compare-only pair test, other sizes
     the direct one; filter widths with threshold-derived indices (fw > ~0.28) and without (0.25);
-    the LDS-staged, four-pixels-per-lane and one-pixel-per-lane kernels."""
+    the four-pixels-per-lane and one-pixel-per-lane kernels."""
     p = _params(glass_scene, 40, 30, 4, bucket_size=bucket, filter_width=fw, bounces=3)
     g = nart_amd.HipRenderer(glass_scene, splat_mode=splat_mode).render(p)
     o = glass_oracle.render(p)

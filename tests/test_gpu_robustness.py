@@ -91,7 +91,7 @@ def test_rayqueue_lds_fallback(gpu, glass_scene, monkeypatch):
     assert _bits_equal(g, oracle.Oracle(glass_scene).render(p))
 
 
-@pytest.mark.parametrize("variant", [0, 1, 3], ids=["rayqueue", "wavefront", "megakernel"])
+@pytest.mark.parametrize("variant", [0, 3], ids=["rayqueue", "megakernel"])
 def test_forced_octree_replay_single_pool_entry(gpu, cornell_scene, monkeypatch, variant):
     """Every query answered by replaying the reference octree search (NART_OCTREE_EXACT=2) with a
     replay pool of ONE entry (NART_OC_POOL=1): every wave that replays contends for the same
