@@ -45,7 +45,7 @@ CONFIGS = {
     "c3": dict(scene=lambda d: scenes.glass_sphere(d), w=1920, h=1080, spp=256, stride=29,
                workload="C3 glassSphere.json 1920x1080 256spp, bucket 16, bounces 10, filterWidth 2, roughening 0.2",
                data="reference scene input/scenes/glassSphere.json (+ sphere.geo, backdrop.geo) packed in assets/"),
-    "c2": dict(scene=lambda d: scenes.cornell(d), w=1920, h=1080, spp=64, stride=29,
+    "c2": dict(scene=lambda d: scenes.cornell(d), w=1920, h=1080, spp=64, stride=7,
                workload="C2 synthesized Lambert Cornell box, one disk light, 1920x1080 64spp, bounces 10",
                data="synthesized scene (nart_amd/scenes.py cornell)"),
     "c4": dict(scene=lambda d: scenes.c4_teapot(d), w=3840, h=2160, spp=512, stride=211,
@@ -58,7 +58,7 @@ CONFIGS = {
                   workload="C4-style environment-lit textured, normal-mapped plastic + rough glass (UV spheres), "
                            "3840x2160 512spp (round-2 C4 scene)",
                   data="synthesized scene + generated sky EXR (nart_amd/scenes.py environment)"),
-    "c5": dict(scene=lambda d: scenes.volume(d, kind="c5"), w=1920, h=1080, spp=1024, stride=59,
+    "c5": dict(scene=lambda d: scenes.volume(d, kind="c5"), w=1920, h=1080, spp=1024, stride=7,
                workload="C5 homogeneous medium (density 1, sigma_s 8), volume integrator, 1920x1080 1024spp, 32 bounces",
                data="synthesized .vol + generated sky EXR (nart_amd/scenes.py volume)"),
 }
@@ -106,19 +106,19 @@ def cpu_baseline(scene, p, ids, stride):
     return out, tiles
 
 
-def load_traffic(tag):
-    """HBM bytes per launch of the render kernel (rocprofv3 FETCH_SIZE + WRITE_SIZE, separate
-    --pmc passes of this bench command: tools/profile.sh + tools/summarize_prof.py) and where
-    the figure comes from.  A bench cannot run rocprofv3 on itself, so the figure is read from
-    the committed summary, and only if that summary was measured on the current kernel sources
-    (hip_source_sha); otherwise traffic is null and the source says why."""
+def load_profile(tag):
+    """The committed rocprofv3 summary of this bench command (tools/profile.sh +
+    tools/summarize_prof.py: FETCH_SIZE x 2 + WRITE_SIZE per launch, SQ lane utilisation), and
+    where it comes from.  A bench cannot run rocprofv3 on itself, so the figures are read from
+    the committed summary, and only if it was measured on the current kernel sources
+    (hip_source_sha); otherwise None and the source says why."""
     from nart_amd.build import hip_source_sha
     path = os.path.join(REPO, "profiles", "pmc_latest.json")
     if not os.path.exists(path):
         return None, "no committed PMC summary"
     try:
         d = json.load(open(path))
-    except Exception as e:
+    except Exception as e:  # noqa: BLE001
         return None, "unreadable PMC summary: %s" % e
     if d.get("config") != tag:
         return None, "PMC summary is for %s, not %s" % (d.get("config"), tag)
@@ -126,8 +126,29 @@ def load_traffic(tag):
     if d.get("hip_source_sha") != sha:
         return None, "PMC summary %s predates the current kernel sources (%s vs %s)" % (
             d.get("profile"), d.get("hip_source_sha"), sha)
-    return d.get("hbm_bytes_per_launch"), "profiles/%s_pmc.json (rocprofv3 FETCH_SIZE + WRITE_SIZE, kernel sources %s)" % (
+    return d, "profiles/%s_pmc.json (rocprofv3: 2 x FETCH_SIZE + WRITE_SIZE, SQ counters; kernel sources %s)" % (
         d.get("profile"), sha)
+
+
+def kernel_ratios(prof, samples, tiles_bytes):
+    """Counter bytes against algorithmic bytes for the splat and the LatinSquare (per launch):
+    splat input 24 B per sample (sample + radiance) + its tiles; LatinSquare 8 B per sample written."""
+    if not prof:
+        return None
+    out = {}
+    for k, e in prof.get("kernels", {}).items():
+        if "hbm_bytes" not in e:
+            continue
+        if "k_splat" in k:
+            alg = 24.0 * samples + tiles_bytes
+        elif "k_latin" in k:
+            alg = 8.0 * samples
+        else:
+            continue
+        out[k] = {"algorithmic_bytes": alg, "counter_bytes": e["hbm_bytes"],
+                  "counter_over_algorithmic": round(e["hbm_bytes"] / alg, 2),
+                  "lane_utilization": e.get("lane_utilization")}
+    return out or None
 
 
 def main():
@@ -234,21 +255,32 @@ def main():
     bps = bytes_per_sample(counters)
     per_launch_samples = st.traced_samples / max(1, st.kernel_launches)
     achieved = bps * per_launch_samples / (kernel_avg_ms * 1e-3) / 1e9
-    traffic, traffic_src = load_traffic("%dx%dx%d" % (W, H, SPP))
-    # achieved/frac price the kernel's ALGORITHMIC bytes (BVH nodes, triangles,
-    # path state per sample) against HBM peak, as the bench contract asks.  Those bytes are
-    # served mostly from LDS/L1/L2 (a ~0.5 MB scene); the kernel is latency/VALU-bound, which
-    # measured_frac (PMC bytes actually moved over HBM / kernel time / peak) shows.
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+    prof, prof_src = load_profile("%dx%dx%d" % (W, H, SPP))
+    traffic = prof.get("hbm_bytes_per_launch") if prof else None
+    # The path kernels are latency/issue-bound, not HBM-bound: achieved/frac price the contract's
+    # ALGORITHMIC bytes (BVH nodes, triangles, rays, path state per sample) against
+    # the HBM ceiling, but those bytes are served from LDS/L1/L2 (a ~0.5 MB scene).  What HBM really
+    # moves is `traffic` (rocprofv3 2 x FETCH_SIZE + WRITE_SIZE per launch) -> measured_frac, and
+    # what limits the kernel shows in lane_utilization (SQ_THREAD_CYCLES_VALU / 64
+    # SQ_ACTIVE_INST_VALU: divergent lanes) and valu_busy.
+    roofline = {"bound": "latency", "ceiling": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                 "achieved_kind": "algorithmic bytes per launch (SURVEY.md 8(d) per-sample model x traced samples)",
-                "limiter": "latency/VALU issue: dependent LDS/L2 loads in BVH traversal, divergent lanes "
+                "limiter": "latency/issue: dependent LDS/L2 loads in BVH traversal and divergent lanes "
                            "(DESIGN.md section 4), not HBM bandwidth",
                 "measured_frac": (round(traffic / (kernel_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
                                   if traffic else None),
-                "traffic_source": traffic_src,
+                "lane_utilization": prof.get("lane_utilization") if prof else None,
+                "valu_busy": prof.get("valu_busy") if prof else None,
+                "traffic_source": prof_src,
                 "kernel": "k_render_volume_sm" if p.integrator == 1 else "k_primary + k_render_rq",
-                "kernel_avg_ms": round(kernel_avg_ms, 3), "bytes_per_sample": round(bps, 1)}
+                "kernel_avg_ms": round(kernel_avg_ms, 3), "bytes_per_sample": round(bps, 1),
+                "rays_per_s": round((counters["rays_extend"] + counters["rays_shadow"]) /
+                                    max(1, counters["traced_samples"]) * per_launch_samples /
+                                    (kernel_avg_ms * 1e-3), 1)}
+    ratios = kernel_ratios(prof, per_launch_samples, nb * tpx * 20.0)
+    if ratios:
+        roofline["other_kernels"] = ratios
     if p.integrator != 1:
         # the path tracing is two launches (camera rays, then the path kernel); the counters and
         # the time above cover both, the rocprofv3 summary lists them separately

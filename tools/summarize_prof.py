@@ -1,13 +1,15 @@
 """Summarise a tools/profile.sh run into profiles/ (committed evidence).
 
-    python tools/summarize_prof.py gpurun_out/prof1 r01
+    python tools/summarize_prof.py gpurun_out/prof1 r03x [config]
 
-writes profiles/<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats summary),
-profiles/<tag>_pmc.json and profiles/pmc_latest.json (HBM bytes per launch per nart kernel).
-FETCH_SIZE / WRITE_SIZE are KiB (rocprofv3); per MI355X_MICROARCH.md (HBM section) FETCH_SIZE
-reads 1/2 of a wide coalesced streaming read on gfx950 -- the render kernels' reads are not
-wide streaming reads (scattered 8/16-B gathers), so both the raw and the x2-corrected read
-figures are recorded and `hbm_bytes_per_launch` uses the raw (uncalibrated) sum.
+writes profiles/<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats summary) and
+profiles/<tag>_pmc.json + profiles/pmc_latest.json: per nart kernel the HBM-side bytes per launch
+(FETCH_SIZE x 2 -- on gfx950 FETCH_SIZE counts half the bytes of a wide read, MI355X_MICROARCH.md
+HBM section -- plus WRITE_SIZE; both rocprofv3 KiB) and the SQ issue counters: VALU busy
+(SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES), SIMD lane utilisation (SQ_THREAD_CYCLES_VALU /
+(64 SQ_ACTIVE_INST_VALU)), waiting and issue-stall fractions.  `hbm_bytes_per_launch` is the
+corrected sum for the path-tracing launch pair (k_primary + k_render_rq) that bench.py's roofline
+times; bench.py reads it only while `hip_source_sha` matches the kernel sources.
 """
 import csv
 import json
@@ -18,56 +20,88 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _key(name):
+    return name.split("(")[0].replace("void ", "")
+
+
+def _rows(src, kind):
+    path = os.path.join(src, kind, "run_counter_collection.csv")
+    return list(csv.DictReader(open(path))) if os.path.exists(path) else []
+
+
 def main(src, tag, config="1920x1080x256"):
     prof = os.path.join(REPO, "profiles")
     os.makedirs(prof, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(prof, tag + "_kernel_stats.csv"))
     per = {}
-    for kind in ("fetch", "write"):
-        for r in csv.DictReader(open(os.path.join(src, kind, "run_counter_collection.csv"))):
-            name = r["Kernel_Name"]
-            if "nd::" not in name:
+    # one dispatch per kernel name: the longest (the timed launch, not a probe / counter pass of
+    # the same template); counters of the same dispatch id across passes
+    for kind in ("fetch", "write", "sq"):
+        for r in _rows(src, kind):
+            if "nd::" not in r["Kernel_Name"]:
                 continue
-            key = name.split("(")[0].replace("void ", "")
-            d = per.setdefault(key, {"launches": {}, "vgpr": r["VGPR_Count"], "sgpr": r["SGPR_Count"],
-                                     "lds": r["LDS_Block_Size"], "scratch": r["Scratch_Size"]})
+            k = _key(r["Kernel_Name"])
+            d = per.setdefault(k, {"vgpr": r.get("VGPR_Count"), "sgpr": r.get("SGPR_Count"),
+                                   "lds": r.get("LDS_Block_Size"), "scratch": r.get("Scratch_Size")})
             dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
-            d["launches"].setdefault(r["Dispatch_Id"] if kind == "fetch" else None, None)
-            d.setdefault(kind, []).append((float(r["Counter_Value"]), dur))
+            disp = d.setdefault(kind, {}).setdefault(r["Dispatch_Id"], {"dur": dur})
+            disp[r["Counter_Name"]] = disp.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     sys.path.insert(0, REPO)
     from nart_amd.build import hip_source_sha
-    # the profiled run's kernels are this tree's (run from the same snapshot)
-    out = {"config": config, "profile": tag, "hip_source_sha": hip_source_sha(), "kernels": {}}
+    out = {"config": config, "profile": tag, "hip_source_sha": hip_source_sha(), "kernels": {},
+           "notes": "fetch_bytes_corrected = 2 x FETCH_SIZE (gfx950), write_bytes = WRITE_SIZE; per launch "
+                    "(the longest dispatch of each kernel)"}
     for k, d in per.items():
-        f = max(d.get("fetch", [(0, 0)]))
-        w = max(d.get("write", [(0, 0)]))
-        out["kernels"][k] = {"fetch_kib": f[0], "write_kib": w[0], "fetch_bytes": f[0] * 1024,
-                             "fetch_bytes_x2_corrected": f[0] * 2048, "write_bytes": w[0] * 1024,
-                             "duration_ms_fetch_pass": f[1], "duration_ms_write_pass": w[1],
-                             "vgpr_count": d["vgpr"], "sgpr_count": d["sgpr"], "lds_bytes": d["lds"],
-                             "scratch_bytes": d["scratch"]}
-    def timed_render(name):  # k_render_rq<MAXL, COUNT, ENV> / k_render<...>: not the counter / cost-probe pass
-        if "k_render_rq<" not in name and "k_render<" not in name:
+        e = {"vgpr_count": d["vgpr"], "sgpr_count": d["sgpr"], "lds_bytes": d["lds"], "scratch_bytes": d["scratch"]}
+        for kind, field in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+            if kind in d:
+                top = max(d[kind].values(), key=lambda v: v["dur"])
+                e[kind + "_kib"] = top.get(field, 0.0)
+                e["duration_ms_" + kind + "_pass"] = top["dur"]
+        if "fetch_kib" in e:
+            e["fetch_bytes_corrected"] = e["fetch_kib"] * 2048
+        if "write_kib" in e:
+            e["write_bytes"] = e["write_kib"] * 1024
+        if "fetch_bytes_corrected" in e and "write_bytes" in e:
+            e["hbm_bytes"] = e["fetch_bytes_corrected"] + e["write_bytes"]
+            dur = e.get("duration_ms_fetch_pass") or 1e-9
+            e["hbm_gbps"] = e["hbm_bytes"] / (dur * 1e-3) / 1e9
+        if "sq" in d:
+            top = max(d["sq"].values(), key=lambda v: v["dur"])
+            wc = top.get("SQ_WAVE_CYCLES", 0.0) or 1.0
+            av = top.get("SQ_ACTIVE_INST_VALU", 0.0)
+            e["sq"] = {n: v for n, v in top.items() if n != "dur"}
+            e["valu_busy"] = av / wc
+            e["lane_utilization"] = top.get("SQ_THREAD_CYCLES_VALU", 0.0) / (64.0 * av) if av else None
+            e["wait_any"] = top.get("SQ_WAIT_ANY", 0.0) / wc
+            e["wait_inst_any"] = top.get("SQ_WAIT_INST_ANY", 0.0) / wc
+        out["kernels"][k] = e
+
+    def timed(name, base):  # k_render_rq<MAXL, COUNT, ENV> / k_primary<COUNT, ENV>: COUNT == false
+        if not name.startswith("nd::" + base + "<"):
             return False
         args = [a.strip() for a in name.split("<", 1)[1].split(">", 1)[0].split(",")]
-        return len(args) >= 2 and args[1] == "false"
+        return "false" == (args[1] if base != "k_primary" else args[0])
 
-    render = sorted((k for k in out["kernels"] if timed_render(k)), key=lambda k: "k_render_rq<" not in k)
-    if render:
-        r = out["kernels"][render[0]]
-        out["hbm_bytes_per_launch"] = r["fetch_bytes"] + r["write_bytes"]
-        out["render_kernel"] = render[0]
-        # the camera-ray kernel runs before the path kernel in the same launch sequence: the bench's
-        # roofline times both, so its HBM traffic counts both
-        prim = [k for k in out["kernels"] if k.startswith("nd::k_primary<false")]
-        if prim and "k_render_rq<" in render[0]:
-            p0 = out["kernels"][prim[0]]
-            out["hbm_bytes_per_launch"] += p0["fetch_bytes"] + p0["write_bytes"]
-            out["render_kernel"] = prim[0] + " + " + render[0]
+    rq = [k for k in out["kernels"] if timed(k, "k_render_rq")]
+    pr = [k for k in out["kernels"] if timed(k, "k_primary")]
+    if rq and "hbm_bytes" in out["kernels"][rq[0]]:
+        r = out["kernels"][rq[0]]
+        out["render_kernel"] = rq[0]
+        out["hbm_bytes_per_launch"] = r["hbm_bytes"]
+        if pr and "hbm_bytes" in out["kernels"][pr[0]]:
+            out["hbm_bytes_per_launch"] += out["kernels"][pr[0]]["hbm_bytes"]
+            out["render_kernel"] = pr[0] + " + " + rq[0]
+        out["lane_utilization"] = r.get("lane_utilization")
+        out["valu_busy"] = r.get("valu_busy")
     json.dump(out, open(os.path.join(prof, tag + "_pmc.json"), "w"), indent=1)
-    json.dump(out, open(os.path.join(prof, "pmc_latest.json"), "w"), indent=1)
-    print(json.dumps(out, indent=1))
+    if config == "1920x1080x256":
+        json.dump(out, open(os.path.join(prof, "pmc_latest.json"), "w"), indent=1)
+    print(json.dumps({k: v for k, v in out.items() if k != "kernels"}, indent=1))
+    for k, e in out["kernels"].items():
+        print("%-44s hbm %8.2f GB  %7.1f GB/s  lane_util %s  valu_busy %s" % (
+            k[:44], e.get("hbm_bytes", 0) / 1e9, e.get("hbm_gbps", 0), e.get("lane_utilization"), e.get("valu_busy")))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], *(sys.argv[3:4]))
