@@ -121,6 +121,11 @@ typedef struct nart_bvh_info {
 } nart_bvh_info;
 int nart_hip_bvh_info(const nart_scene_blob* scene, nart_bvh_info* out);
 
+/* The acceleration structure a context built: nodes, stack depth, leaf triangles; reserved = 1
+   when it was built on the device (NART_BVH_BUILD=device: a linear BVH, device/lbvh.h; default
+   the host's binned SAH), and the build time in ms (host wall clock, uploads included). */
+int nart_hip_context_bvh(const nart_ctx* ctx, nart_bvh_info* out, double* build_ms);
+
 /* Kernel variant (all render bit-identical images):
    0 = megakernel with a wave ray queue (default; one lane per pixel slot, the lanes of a wave
        trace each other's queued shadow and continuation rays; scenes whose BVH stack does not fit

@@ -124,6 +124,7 @@ _HIP_SIGS = {
     "nart_hip_create_multi": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(_P)]),
     "nart_hip_context_devices": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "nart_hip_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "nart_hip_context_bvh": (ctypes.c_int, [_P, ctypes.POINTER(BvhInfo), ctypes.POINTER(ctypes.c_double)]),
     "nart_hip_shard_buckets": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                               ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
 }
@@ -342,6 +343,13 @@ class HipRenderer:
     def _check(self, rc):
         if rc != NART_OK:
             raise NartError(rc, self._lib.nart_hip_last_error(self._ctx).decode())
+
+    def bvh(self):
+        """The acceleration structure this context built (nart_hip_context_bvh)."""
+        info, ms = BvhInfo(), ctypes.c_double()
+        self._check(self._lib.nart_hip_context_bvh(self._ctx, ctypes.byref(info), ctypes.byref(ms)))
+        return {"num_nodes": info.num_nodes, "stack_depth": info.stack_depth, "num_leaf_tris": info.num_leaf_tris,
+                "on_device": bool(info.reserved), "build_ms": ms.value}
 
     def devices(self):
         """(number of devices, gather over RCCL) of this context."""

@@ -470,14 +470,11 @@ void build_bvh(const nart_scene_blob& blob, const std::vector<uint8_t>& mask, fl
 // it whose ray is not grazing (|dot(d, n)| >= |n| / 8, word 15; the plane distance t then places
 // o + t d within ~250 ulps of the scene scale of the triangle) is clear of the leaf's faces,
 // and octree.h needs no box loads for it.
-void annotate_octree_leaves(const nart_scene_blob& blob, const RefOctree& oct, float margin, BuiltBVH& bvh) {
-    const size_t n = bvh.tri_isect.size() / 16;
-    for (size_t i = 0; i < n; ++i) {
-        float* r = &bvh.tri_isect[i * 16];
-        uint32_t g;
-        std::memcpy(&g, &r[13], 4);
+void octree_leaf_info(const nart_scene_blob& blob, const RefOctree& oct, float margin, std::vector<uint32_t>& info) {
+    info.assign(blob.num_triangles, 0u);
+    for (uint32_t g = 0; g < blob.num_triangles; ++g) {
         const int32_t leaf = g < oct.tri_leaf.size() ? oct.tri_leaf[g] : -1;
-        uint32_t info = leaf >= 0 ? (uint32_t)leaf : 0u;
+        uint32_t v = leaf >= 0 ? (uint32_t)leaf : 0u;
         if (leaf >= 0) {
             const nd::OcNode& L = oct.nodes[leaf];
             const nart_triangle& T = blob.triangles[g];
@@ -487,9 +484,21 @@ void annotate_octree_leaves(const nart_scene_blob& blob, const RefOctree& oct, f
                 const float hi = std::max(T.v0[k], std::max(T.v1[k], T.v2[k]));
                 inside = L.bmin[k] < L.bmax[k] && lo - L.bmin[k] >= margin && L.bmax[k] - hi >= margin;
             }
-            if (inside) info |= 0x80000000u;
+            if (inside) v |= 0x80000000u;
         }
-        std::memcpy(&r[14], &info, 4);
+        info[g] = v;
+    }
+}
+
+void annotate_octree_leaves(const nart_scene_blob& blob, const RefOctree& oct, float margin, BuiltBVH& bvh) {
+    std::vector<uint32_t> info;
+    octree_leaf_info(blob, oct, margin, info);
+    const size_t n = bvh.tri_isect.size() / 16;
+    for (size_t i = 0; i < n; ++i) {
+        float* r = &bvh.tri_isect[i * 16];
+        uint32_t g;
+        std::memcpy(&g, &r[13], 4);
+        std::memcpy(&r[14], &info[g], 4);
     }
 }
 

@@ -43,4 +43,7 @@ void build_bvh(const nart_scene_blob& blob, const std::vector<uint8_t>& mask, fl
 // `margin` (device/octree.h fast path).
 void annotate_octree_leaves(const nart_scene_blob& blob, const RefOctree& oct, float margin, BuiltBVH& bvh);
 
+// The same tag for every scene triangle (info[g]), for the device-side build (device/lbvh.h).
+void octree_leaf_info(const nart_scene_blob& blob, const RefOctree& oct, float margin, std::vector<uint32_t>& info);
+
 }  // namespace nart

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/nart_hip.h"
+#include "device/lbvh.h"
 #include "device/volume.h"
 #include "host/bvh_build.h"
 
@@ -86,6 +87,10 @@ struct nart_ctx {
     std::vector<size_t> sub_cap;
     std::vector<ncclComm_t> comms;
     bool gather_rccl = false;
+    // acceleration structure: built on the device (NART_BVH_BUILD=device) or the host; build time
+    bool bvh_on_device = false;
+    double bvh_ms = 0.0;
+    uint32_t num_leaf_tris = 0;
     void *d_gather = nullptr, *d_byid = nullptr, *d_image = nullptr;
     size_t cap_gather = 0, cap_byid = 0, cap_image = 0;
 };
@@ -1079,6 +1084,117 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
     return NART_OK;
 }
 
+// ---------------------------------------------------------------- device-side BVH build
+struct LbvhResult {
+    uint32_t max_stack = 1, num_nodes = 0, num_leaf_tris = 0;
+    int32_t root_code = -1;
+};
+
+// Linear BVH on the device (device/lbvh.h) over the triangles the reference octree can return
+// (mask), into ctx->d_nodes / d_tri_isect / d_tri_perm.  ctx->d_tris must be resident.
+int build_bvh_device(nart_ctx* ctx, const nart_scene_blob& blob, const std::vector<uint8_t>& mask,
+                     const nart::RefOctree& oct, float pad, float margin, LbvhResult& out) {
+    std::vector<uint32_t> vis, info;
+    for (uint32_t g = 0; g < blob.num_triangles; ++g)
+        if (mask[g]) vis.push_back(g);
+    nart::octree_leaf_info(blob, oct, margin, info);
+    const uint32_t m = (uint32_t)vis.size();
+    out.num_leaf_tris = m;
+    if (m == 0) {  // nothing the octree can return: never traversed (geometry_visible = 0)
+        BVHNode dummy{};
+        int rc = upload(ctx, ctx->d_nodes, &dummy, 0);
+        if (!rc) rc = upload(ctx, ctx->d_tri_isect, (const float*)nullptr, 0);
+        if (!rc) rc = upload(ctx, ctx->d_tri_perm, (const float*)nullptr, 0);
+        return rc;
+    }
+    const int n = (int)((m + LBVH_LEAF - 1) / LBVH_LEAF);  // leaves
+    const int ninner = n - 1;
+    std::vector<void*> tmp;
+    auto alloc = [&](void** p, size_t bytes) {
+        const int rc = dmalloc(ctx, p, bytes ? bytes : 4, "BVH build scratch");
+        if (!rc) tmp.push_back(*p);
+        return rc;
+    };
+    auto cleanup = [&](int rc) {
+        for (void* p : tmp) hipFree(p);
+        return rc;
+    };
+    uint32_t *d_vis, *d_info, *d_keys[2], *d_vals[2], *d_lkey, *d_flag, *d_maxd, *d_ord[2];
+    LbvhPrim *d_prims, *d_sorted;
+    float* d_part;
+    int2* d_child;
+    int *d_pin, *d_pleaf, *d_remap;
+    LbvhBox* d_box;
+    const uint32_t nb = std::min<uint32_t>(1024, (m + 255) / 256);
+    const size_t ni = (size_t)std::max(ninner, 1);
+    int rc = NART_OK;
+    if ((rc = alloc((void**)&d_vis, m * 4)) || (rc = alloc((void**)&d_info, blob.num_triangles * 4)) ||
+        (rc = alloc((void**)&d_prims, m * sizeof(LbvhPrim))) || (rc = alloc((void**)&d_sorted, m * sizeof(LbvhPrim))) ||
+        (rc = alloc((void**)&d_part, nb * 6 * 4)) || (rc = alloc((void**)&d_keys[0], m * 4)) ||
+        (rc = alloc((void**)&d_keys[1], m * 4)) || (rc = alloc((void**)&d_vals[0], m * 4)) ||
+        (rc = alloc((void**)&d_vals[1], m * 4)) || (rc = alloc((void**)&d_lkey, n * 4)) ||
+        (rc = alloc((void**)&d_child, ni * sizeof(int2))) || (rc = alloc((void**)&d_pin, ni * 4)) ||
+        (rc = alloc((void**)&d_pleaf, (size_t)n * 4)) || (rc = alloc((void**)&d_box, ni * sizeof(LbvhBox))) ||
+        (rc = alloc((void**)&d_flag, ni * 4)) || (rc = alloc((void**)&d_maxd, 4)) ||
+        (rc = alloc((void**)&d_ord[0], ni * 4)) || (rc = alloc((void**)&d_ord[1], ni * 4)) ||
+        (rc = alloc((void**)&d_remap, ni * 4)))
+        return cleanup(rc);
+    if (hipMemcpy(d_vis, vis.data(), m * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_info, info.data(), blob.num_triangles * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(d_pin, 0xFF, ni * 4) != hipSuccess || hipMemset(d_pleaf, 0xFF, (size_t)n * 4) != hipSuccess ||
+        hipMemset(d_flag, 0, ni * 4) != hipSuccess || hipMemset(d_maxd, 0, 4) != hipSuccess)
+        return cleanup(fail(ctx, NART_E_HIP, "BVH build: upload"));
+    const dim3 blk(256);
+    const uint32_t gm = (m + 255) / 256, gn = ((uint32_t)n + 255) / 256, gi = ((uint32_t)ni + 255) / 256;
+    hipLaunchKernelGGL(k_lbvh_prims, dim3(gm), blk, 0, 0, (const nart_triangle*)ctx->d_tris, d_vis, m, d_prims);
+    hipLaunchKernelGGL(k_lbvh_bounds, dim3(nb), blk, 0, 0, d_prims, m, d_part);
+    hipLaunchKernelGGL(k_lbvh_bounds_final, dim3(1), dim3(64), 0, 0, d_part, nb);
+    hipLaunchKernelGGL(k_lbvh_morton, dim3(gm), blk, 0, 0, d_prims, m, d_part, d_keys[0], d_vals[0]);
+    size_t ts = 0;
+    if (hipcub::DeviceRadixSort::SortPairs(nullptr, ts, d_keys[0], d_keys[1], d_vals[0], d_vals[1], (int)m, 0, 30) !=
+        hipSuccess)
+        return cleanup(fail(ctx, NART_E_HIP, "BVH build: sort size"));
+    void* d_ts = nullptr;
+    if ((rc = alloc(&d_ts, ts))) return cleanup(rc);
+    if (hipcub::DeviceRadixSort::SortPairs(d_ts, ts, d_keys[0], d_keys[1], d_vals[0], d_vals[1], (int)m, 0, 30) !=
+        hipSuccess)
+        return cleanup(fail(ctx, NART_E_HIP, "BVH build: sort"));
+    hipLaunchKernelGGL(k_lbvh_gather, dim3(gm), blk, 0, 0, d_prims, d_vals[1], m, d_sorted);
+    hipLaunchKernelGGL(k_lbvh_leaf_keys, dim3(gn), blk, 0, 0, d_keys[1], m, n, d_lkey);
+    if (ninner > 0) {
+        hipLaunchKernelGGL(k_lbvh_karras, dim3(gi), blk, 0, 0, d_lkey, n, d_child, d_pin, d_pleaf);
+        hipLaunchKernelGGL(k_lbvh_refit, dim3(gn), blk, 0, 0, d_sorted, m, n, d_child, d_pin, d_pleaf, d_box, d_flag);
+        hipLaunchKernelGGL(k_lbvh_depth, dim3(gi), blk, 0, 0, d_pin, ninner, d_keys[0], d_vals[0], d_maxd);
+        size_t ts2 = 0;
+        if (hipcub::DeviceRadixSort::SortPairs(nullptr, ts2, d_keys[0], d_keys[1], d_vals[0], d_ord[0], ninner, 0, 8) !=
+            hipSuccess)
+            return cleanup(fail(ctx, NART_E_HIP, "BVH build: sort size"));
+        void* d_ts2 = nullptr;
+        if ((rc = alloc(&d_ts2, ts2))) return cleanup(rc);
+        if (hipcub::DeviceRadixSort::SortPairs(d_ts2, ts2, d_keys[0], d_keys[1], d_vals[0], d_ord[0], ninner, 0, 8) !=
+            hipSuccess)
+            return cleanup(fail(ctx, NART_E_HIP, "BVH build: sort"));
+        hipLaunchKernelGGL(k_lbvh_remap, dim3(gi), blk, 0, 0, d_ord[0], ninner, d_remap);
+    }
+    if ((rc = dmalloc(ctx, &ctx->d_nodes, ni * sizeof(BVHNode), "BVH nodes")) ||
+        (rc = dmalloc(ctx, &ctx->d_tri_isect, (size_t)m * 64, "triangle records")) ||
+        (rc = dmalloc(ctx, &ctx->d_tri_perm, (size_t)m * 64 * 3, "permuted triangle records")))
+        return cleanup(rc);
+    if (ninner > 0)
+        hipLaunchKernelGGL(k_lbvh_emit, dim3(gi), blk, 0, 0, d_ord[0], ninner, d_child, d_remap, d_box, d_sorted, m, pad,
+                           (BVHNode*)ctx->d_nodes);
+    hipLaunchKernelGGL(k_lbvh_tris, dim3(gm), blk, 0, 0, (const nart_triangle*)ctx->d_tris, d_sorted, m, d_info,
+                       (float*)ctx->d_tri_isect);
+    hipLaunchKernelGGL(k_lbvh_perm, dim3(gm), blk, 0, 0, (const float*)ctx->d_tri_isect, m, (float*)ctx->d_tri_perm);
+    uint32_t maxd = 0;
+    if (hipGetLastError() != hipSuccess || hipMemcpy(&maxd, d_maxd, 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return cleanup(fail(ctx, NART_E_HIP, "BVH build: kernels"));
+    out.num_nodes = (uint32_t)std::max(ninner, 0);
+    out.max_stack = ninner > 0 ? maxd + 1 : 1;
+    out.root_code = ninner > 0 ? 0 : ~(int32_t)(m - 1);  // one leaf of m <= LBVH_LEAF triangles
+    return cleanup(NART_OK);
+}
+
 }  // namespace
 
 #include "host/multi_gpu.h"
@@ -1128,17 +1244,28 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     }
     for (int k = 12; k < 15; ++k) maxabs = std::max(maxabs, std::fabs(blob->camera.m[k]));
     for (int k = 3; k < 16; k += 4) maxabs = std::max(maxabs, std::fabs(blob->camera.m[k]));
-    nart::BuiltBVH bvh;
-    nart::build_bvh(*blob, mask, maxabs * 6.103515625e-05f + 1e-6f, bvh);
     // hit points deviate from the reference's slab arithmetic by far less than 2^-14 * scene
     // scale (|o| + |t d| <= 3 * maxabs, errors of a few ulps): octree.h oc_clear
-    nart::annotate_octree_leaves(*blob, oct, maxabs * 6.103515625e-05f, bvh);
-    ctx->stack_depth = std::max<uint32_t>(bvh.max_stack + 1, 2);
-    if ((size_t)ctx->stack_depth * 256 * 8 > (size_t)160 * 1024) return bail(NART_E_UNSUPPORTED);  // LDS stack
-    if ((rc = upload(ctx, ctx->d_nodes, bvh.nodes.data(), bvh.nodes.size()))) return bail(rc);
-    ctx->num_nodes = (uint32_t)bvh.nodes.size();
-    if ((rc = upload(ctx, ctx->d_tri_isect, bvh.tri_isect.data(), bvh.tri_isect.size()))) return bail(rc);
-    {
+    const float pad = maxabs * 6.103515625e-05f + 1e-6f, margin = maxabs * 6.103515625e-05f;
+    if ((rc = upload(ctx, ctx->d_tris, blob->triangles, blob->num_triangles))) return bail(rc);
+    // NART_BVH_BUILD=device: linear BVH built on the GPU (device/lbvh.h); default: binned SAH on
+    // the host (host/bvh_build.cpp) -- same node / record format, same images
+    const char* bb = std::getenv("NART_BVH_BUILD");
+    ctx->bvh_on_device = bb && std::string(bb) == "device";
+    const auto tb0 = std::chrono::steady_clock::now();
+    LbvhResult lb;
+    if (ctx->bvh_on_device) {
+        if ((rc = build_bvh_device(ctx, *blob, mask, oct, pad, margin, lb))) return bail(rc);
+    } else {
+        nart::BuiltBVH bvh;
+        nart::build_bvh(*blob, mask, pad, bvh);
+        nart::annotate_octree_leaves(*blob, oct, margin, bvh);
+        lb.max_stack = bvh.max_stack;
+        lb.num_nodes = (uint32_t)bvh.nodes.size();
+        lb.root_code = bvh.root_code;
+        lb.num_leaf_tris = (uint32_t)(bvh.tri_isect.size() / 16);
+        if ((rc = upload(ctx, ctx->d_nodes, bvh.nodes.data(), bvh.nodes.size()))) return bail(rc);
+        if ((rc = upload(ctx, ctx->d_tri_isect, bvh.tri_isect.data(), bvh.tri_isect.size()))) return bail(rc);
         // vertex block of every triangle test record, permuted for each ray major axis, followed
         // by the plane {n, dot(v0, n)}: one 64-B record, so a test issues its four loads at once
         const size_t nt = bvh.tri_isect.size() / 16;
@@ -1162,7 +1289,11 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
         }
         if ((rc = upload(ctx, ctx->d_tri_perm, perm.data(), perm.size()))) return bail(rc);
     }
-    if ((rc = upload(ctx, ctx->d_tris, blob->triangles, blob->num_triangles))) return bail(rc);
+    ctx->bvh_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count();
+    ctx->stack_depth = std::max<uint32_t>(lb.max_stack + 1, 2);
+    if ((size_t)ctx->stack_depth * 256 * 8 > (size_t)160 * 1024) return bail(NART_E_UNSUPPORTED);  // LDS stack
+    ctx->num_nodes = lb.num_nodes;
+    ctx->num_leaf_tris = lb.num_leaf_tris;
     std::vector<uint32_t> tri_mesh(blob->num_triangles);
     std::vector<DMesh> meshes(blob->num_meshes);
     for (uint32_t m = 0; m < blob->num_meshes; ++m) {
@@ -1232,9 +1363,9 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     if ((rc = build_medium(ctx, blob->medium, S.medium))) return bail(rc);
     S.num_lights = blob->num_lights;
     S.num_tris = blob->num_triangles;
-    S.num_leaf_tris = (uint32_t)(bvh.tri_isect.size() / 16);
-    S.root = bvh.root_code;
-    S.geometry_visible = (!root_leaf && bvh.num_leaf_tris > 0) ? 1 : 0;
+    S.num_leaf_tris = lb.num_leaf_tris;
+    S.root = lb.root_code;
+    S.geometry_visible = (!root_leaf && lb.num_leaf_tris > 0) ? 1 : 0;
     std::memcpy(S.cam_m, blob->camera.m, sizeof(S.cam_m));
     // glm::tan(glm::radians(fov)) with the host libm, as the reference (pinholecamera.cpp:20)
     S.cam_tan = std::tan(blob->camera.fov * (float)0.01745329251994329576923690768489);
@@ -1536,6 +1667,17 @@ int nart_hip_eval_sincos(nart_ctx* ctx, const float* x, uint32_t n, float* s, fl
     hipFree(dx);
     hipFree(ds);
     hipFree(dc);
+    return NART_OK;
+}
+
+int nart_hip_context_bvh(const nart_ctx* ctx, nart_bvh_info* out, double* build_ms) {
+    if (!ctx || !out) return NART_E_INVALID;
+    const nart_ctx* c = ctx->subs.empty() ? ctx : ctx->subs[0];
+    out->num_nodes = c->num_nodes;
+    out->stack_depth = c->stack_depth;
+    out->num_leaf_tris = c->num_leaf_tris;
+    out->reserved = c->bvh_on_device ? 1u : 0u;
+    if (build_ms) *build_ms = c->bvh_ms;
     return NART_OK;
 }
 
