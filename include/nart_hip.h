@@ -109,6 +109,11 @@ int nart_hip_eval_sincos(nart_ctx* ctx, const float* x, uint32_t n, float* sin_o
    them (the splat then evaluates sqrt and division per pair). */
 int nart_hip_splat_thresholds(float filter_width, float* thr65);
 
+/* Splat filter weight by d2 cell (host only): cell c holds the floats whose bits >> 16 equal
+   b0 + c, as {threshold t, weight below t, weight at or above t, 0} (at most one threshold per
+   cell), cells4 with room for 2048 cells.  NART_E_INVALID where the thresholds do not apply. */
+int nart_hip_splat_lut(float filter_width, float* cells4, uint32_t* n_cells, uint32_t* b0);
+
 /* Acceleration structure the context would build for a scene (host only, no device): BVH2 node
    count, traversal stack depth (levels; the device keeps 8 B per level per lane in LDS) and the
    triangles in leaves.  Deep trees are capped (median splits past 40 levels), so stack_depth

@@ -120,6 +120,8 @@ _HIP_SIGS = {
     "nart_hip_set_variant": (ctypes.c_int, [_P, ctypes.c_int]),
     "nart_hip_set_splat_mode": (ctypes.c_int, [_P, ctypes.c_int]),
     "nart_hip_splat_thresholds": (ctypes.c_int, [ctypes.c_float, _P]),
+    "nart_hip_splat_lut": (ctypes.c_int, [ctypes.c_float, _P, ctypes.POINTER(ctypes.c_uint32),
+                                          ctypes.POINTER(ctypes.c_uint32)]),
     "nart_hip_bvh_info": (ctypes.c_int, [_P, ctypes.POINTER(BvhInfo)]),
     "nart_hip_create_multi": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(_P)]),
     "nart_hip_context_devices": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),

@@ -1449,7 +1449,12 @@ struct SplatArgs {
     uint32_t n_buckets, spp, B, fb, tile, nbx, totalW, totalH;
     float fw;
     float invB, invFw;            // exact reciprocals when B / fw are powers of two, else 0
+    // filter weight by d2 cell (splat_lut): cell = clamp((bits(d2) >> 16) - lut_b0, 0, lut_n - 1),
+    // {threshold, weight below, weight at or above, -}; null when the table does not apply
+    const float4* lut = nullptr;
+    uint32_t lut_b0 = 0, lut_n = 0;
 };
+#define SPLAT_LUT_MAX 2048
 
 // a / b, or a * (1/b) when 1/b is an exact power of two (bit-identical, avoids the
 // correctly-rounded division sequence)
@@ -1660,12 +1665,16 @@ __global__ __launch_bounds__(256) void k_splat(SplatArgs A) {
 // (source pixel raster, sample) order.  Per-sample work (position, bucket-edge tests, the
 // column test and x distance) is shared.  (Four horizontal pixels per lane measured slower:
 // lanes then read source pixels four apart and the L1 misses rose by a third.)
-template <int NP>
+typedef float nd_f2v __attribute__((ext_vector_type(2)));  // packed-math pairs (v_pk_mul/add_f32)
+template <int NP, bool LUT>
 __global__ __launch_bounds__(256) void k_splat_col4(SplatArgs A) {
     __shared__ float s_table[64];
     __shared__ float s_thr[65];
+    __shared__ float4 s_lut[LUT ? SPLAT_LUT_MAX : 1];
     if (threadIdx.x < 64) s_table[threadIdx.x] = A.table[threadIdx.x];
     if (threadIdx.x < 65) s_thr[threadIdx.x] = A.thr[threadIdx.x];
+    if (LUT)
+        for (uint32_t i = threadIdx.x; i < A.lut_n; i += blockDim.x) s_lut[i] = A.lut[i];
     __syncthreads();
     const uint32_t gpc = (A.tile + NP - 1) / NP, lpb = A.tile * gpc;  // lane groups per tile column / bucket
     const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1706,11 +1715,17 @@ __global__ __launch_bounds__(256) void k_splat_col4(SplatArgs A) {
     const float xsA = (float)(tx + x0), xsB = (float)(tx + x0 + A.B);
     const float ysA0 = (float)(ty0 + y0), ysB0 = (float)(ty0 + y0 + A.B);
     const float edgeX = (float)(x0 + A.B + A.fb), edgeY = (float)(y0 + A.B + A.fb);
-    float c[NP][5];
+    // accumulators: {contribution.xy}, {contribution.zw} as packed pairs, and the weight sum (the
+    // same IEEE products and sums per channel as five scalar ones: bit-identical)
+    nd_f2v cxy[NP], czw[NP];
+    float cws[NP];
 #pragma unroll
-    for (int j = 0; j < NP; ++j)
-#pragma unroll
-        for (int k = 0; k < 5; ++k) c[j][k] = 0.f;
+    for (int j = 0; j < NP; ++j) {
+        cxy[j] = nd_f2v{0.f, 0.f};
+        czw[j] = nd_f2v{0.f, 0.f};
+        cws[j] = 0.f;
+    }
+    const int lut_b0 = (int)A.lut_b0, lut_last = (int)A.lut_n - 1;
     for (int ri = 0; ri < nrow; ++ri) {
         const int sy = (ulo + ri <= uhi) ? ulo + ri : bh - 1;
         bool act[NP];
@@ -1738,17 +1753,24 @@ __global__ __launch_bounds__(256) void k_splat_col4(SplatArgs A) {
                     const bool hit = xhit && loy < ys + 1.f && ys < hiy;
                     const float distY = (ys + 0.5f) - scy;
                     const float d2 = dx2 + distY * distY;  // = distX^2 + distY^2 (IEEE + commutes)
-                    int g = (int)(__builtin_amdgcn_sqrtf(d2) * A.idx_scale);
-                    g = g < 0 ? 0 : (g > 63 ? 63 : g);
-                    const float t0 = s_thr[g], t1 = s_thr[g + 1];
-                    const int fi = g - (d2 < t0 ? 1 : 0) + (d2 >= t1 ? 1 : 0);
-                    const float w = s_table[fi];
+                    float w;
+                    if (LUT) {  // one LDS read: the d2 cell's threshold and the weights on either side
+                        int cell = (int)(__float_as_uint(d2) >> 16) - lut_b0;
+                        cell = cell < 0 ? 0 : (cell > lut_last ? lut_last : cell);
+                        const float4 e = s_lut[cell];
+                        w = d2 >= e.x ? e.z : e.y;
+                    } else {
+                        int g = (int)(__builtin_amdgcn_sqrtf(d2) * A.idx_scale);
+                        g = g < 0 ? 0 : (g > 63 ? 63 : g);
+                        const float t0 = s_thr[g], t1 = s_thr[g + 1];
+                        const int fi = g - (d2 < t0 ? 1 : 0) + (d2 >= t1 ? 1 : 0);
+                        w = s_table[fi];
+                    }
                     if (hit) {
-                        c[j][0] += L.x * w;
-                        c[j][1] += L.y * w;
-                        c[j][2] += L.z * w;
-                        c[j][3] += L.w * w;
-                        c[j][4] += w;
+                        const nd_f2v w2 = nd_f2v{w, w};
+                        cxy[j] += nd_f2v{L.x, L.y} * w2;
+                        czw[j] += nd_f2v{L.z, L.w} * w2;
+                        cws[j] += w;
                     }
                 }
             };
@@ -1793,8 +1815,11 @@ __global__ __launch_bounds__(256) void k_splat_col4(SplatArgs A) {
     for (int j = 0; j < NP; ++j) {
         if (!val[j]) continue;
         float* o = A.tiles + ((uint64_t)bi * tpx + (ty0 + j) * A.tile + tx) * 5;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) o[k] = c[j][k];
+        o[0] = cxy[j].x;
+        o[1] = cxy[j].y;
+        o[2] = czw[j].x;
+        o[3] = czw[j].y;
+        o[4] = cws[j];
     }
 }
 

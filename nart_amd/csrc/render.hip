@@ -64,6 +64,7 @@ struct nart_ctx {
     uint32_t* d_bucket_ids = nullptr;
     uint32_t* d_bucket_base = nullptr;
     float* d_table = nullptr;
+    void* d_lut = nullptr;       // splat filter-weight cells (splat_lut)
     unsigned long long* d_counters = nullptr;
     size_t cap_slots = 0, cap_samples = 0, cap_buckets = 0;
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // ev[4]: after k_primary
@@ -826,6 +827,43 @@ bool splat_thresholds(float fw, float thr[65]) {
     return true;
 }
 
+// Filter weight by d2 cell for the splat (k_splat_col4<.., true>): cell c covers the floats whose
+// bits >> 16 equal b0 + c (128 cells per octave of d2).  Consecutive thresholds differ by at
+// least a factor (64/63)^2 = 1.03 > 1 + 1/128, so a cell holds at most one threshold t: the
+// filter index in the cell is base + (d2 >= t), base = fi(cell start).  Cell 0 lies wholly below
+// thr[1] (index 0 for every smaller d2 too); the last cell starts past thr[63] (index 63 beyond).
+// Stored per cell: {t (or inf), table[base], table[base + 1]}.  Returns false when the thresholds
+// do not apply (then the splat keeps the sqrt estimate) or a cell would hold two of them.
+bool splat_lut(const float thr[65], const float table[64], std::vector<float4>& lut, uint32_t& b0) {
+    uint32_t u1, u63;
+    std::memcpy(&u1, &thr[1], 4);
+    std::memcpy(&u63, &thr[63], 4);
+    if (!(thr[1] > 0.f) || !(thr[63] < __builtin_inff())) return false;
+    b0 = (u1 >> 16) - 1;
+    const uint32_t last = (u63 >> 16) + 1;
+    const uint32_t n = last - b0 + 1;
+    if (n > SPLAT_LUT_MAX) return false;
+    lut.assign(n, make_float4(0.f, 0.f, 0.f, 0.f));
+    for (uint32_t c = 0; c < n; ++c) {
+        const uint32_t lo = (b0 + c) << 16, hi = lo | 0xFFFFu;
+        float flo, fhi;
+        std::memcpy(&flo, &lo, 4);
+        std::memcpy(&fhi, &hi, 4);
+        uint32_t base = 0, inside = 0;
+        float t = __builtin_inff();
+        for (uint32_t k = 1; k < 64; ++k) {
+            if (thr[k] <= flo) base = k;
+            else if (thr[k] <= fhi) {
+                ++inside;
+                t = thr[k];
+            }
+        }
+        if (inside > 1) return false;
+        lut[c] = make_float4(t, table[std::min(base, 63u)], table[std::min(base + inside, 63u)], 0.f);
+    }
+    return true;
+}
+
 // LatinSquare per traced pixel: float arrays in LDS up to 256 spp, LDS index shuffles up to 1024
 // spp (scratch in Lout: 2*spp floats per lane of every launched block, within Lout's 4*spp per
 // slot once there are >= 64 slots), the global-memory variant beyond.
@@ -861,6 +899,14 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
     const bool thr_ok = splat_thresholds(p->filter_width, table + 64);
     if (!ctx->d_table) HIPCHK(hipMalloc(&ctx->d_table, sizeof(table)));
     HIPCHK(hipMemcpy(ctx->d_table, table, sizeof(table), hipMemcpyHostToDevice));
+    std::vector<float4> lut;
+    uint32_t lut_b0 = 0;
+    static const bool lut_env = !(std::getenv("NART_SPLAT_LUT") && std::getenv("NART_SPLAT_LUT")[0] == '0');
+    const bool lut_ok = lut_env && thr_ok && splat_lut(table + 64, table, lut, lut_b0);
+    if (lut_ok) {
+        if (!ctx->d_lut) HIPCHK(hipMalloc(&ctx->d_lut, SPLAT_LUT_MAX * sizeof(float4)));
+        HIPCHK(hipMemcpy(ctx->d_lut, lut.data(), lut.size() * sizeof(float4), hipMemcpyHostToDevice));
+    }
 #ifdef NART_WAVEPROF
     const size_t n_cnt = 24 + 8 * 70000 + 4200000;  // + per-wave and per-slot records (development profile)
 #else
@@ -952,6 +998,9 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         sa.totalH = g.total_height;
         sa.fw = p->filter_width;
         sa.invB = (p->bucket_size & (p->bucket_size - 1)) == 0 ? 1.f / (float)p->bucket_size : 0.f;
+        sa.lut = lut_ok ? static_cast<const float4*>(ctx->d_lut) : nullptr;
+        sa.lut_b0 = lut_b0;
+        sa.lut_n = (uint32_t)lut.size();
         {
             int ex = 0;
             float m = std::frexp(p->filter_width, &ex);
@@ -967,7 +1016,14 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         // splat modes (all bit-identical, mode 3 the default): 3 four tile pixels per lane; 2 / 1 / 0
         // one tile pixel per lane with the compare-only / threshold / direct filter-index arithmetic
         if (sa.thr && sa.invB != 0.f && splat_mode >= 3)
-            hipLaunchKernelGGL(k_splat_col4<NART_SPLAT_NP>, dim3((uint32_t)((n4 + 255) / 256)), dim3(256), 0, st, sa);
+        {
+            if (sa.lut)
+                hipLaunchKernelGGL((k_splat_col4<NART_SPLAT_NP, true>), dim3((uint32_t)((n4 + 255) / 256)), dim3(256), 0,
+                                   st, sa);
+            else
+                hipLaunchKernelGGL((k_splat_col4<NART_SPLAT_NP, false>), dim3((uint32_t)((n4 + 255) / 256)), dim3(256),
+                                   0, st, sa);
+        }
         else if (sa.thr && sa.invB != 0.f && splat_mode >= 2) hipLaunchKernelGGL(k_splat<2>, sg, dim3(256), 0, st, sa);
         else if (sa.thr && splat_mode >= 1) hipLaunchKernelGGL(k_splat<1>, sg, dim3(256), 0, st, sa);
         else hipLaunchKernelGGL(k_splat<0>, sg, dim3(256), 0, st, sa);
@@ -1419,7 +1475,7 @@ void nart_hip_destroy(nart_ctx* ctx) {
     hipSetDevice(ctx->device);
     void* bufs[] = {ctx->d_nodes, ctx->d_tri_isect, ctx->d_tri_perm, ctx->d_tris, ctx->d_tri_mesh, ctx->d_meshes, ctx->d_mats,
                     ctx->d_lights, ctx->d_texs, ctx->d_tex_pool, ctx->d_slot_xy, ctx->d_slot_so, ctx->d_rng, ctx->d_samples, ctx->d_prim,
-                    ctx->d_L, ctx->d_bucket_ids, ctx->d_bucket_base, ctx->d_table, ctx->d_counters, ctx->d_envs, ctx->d_density,
+                    ctx->d_L, ctx->d_bucket_ids, ctx->d_bucket_base, ctx->d_table, ctx->d_lut, ctx->d_counters, ctx->d_envs, ctx->d_density,
                     ctx->d_oc_nodes, ctx->d_oc_chunks, ctx->d_oc_tris, ctx->d_tri_leaf, ctx->d_oc_lock, ctx->d_oc_heap,
                     ctx->d_queue, ctx->d_cost, ctx->d_keys[0], ctx->d_keys[1], ctx->d_vals[0], ctx->d_vals[1],
                     ctx->d_qhead, ctx->d_sort_tmp};
@@ -1643,6 +1699,17 @@ int nart_hip_bvh_info(const nart_scene_blob* blob, nart_bvh_info* out) {
     out->stack_depth = std::max<uint32_t>(bvh.max_stack + 1, 2);  // as nart_hip_create
     out->num_leaf_tris = bvh.num_leaf_tris;
     out->reserved = 0;
+    return NART_OK;
+}
+
+int nart_hip_splat_lut(float filter_width, float* cells4, uint32_t* n_cells, uint32_t* b0) {
+    if (!cells4 || !n_cells || !b0) return NART_E_INVALID;
+    float table[64 + 65];
+    nart_filter_table(table);
+    std::vector<float4> lut;
+    if (!splat_thresholds(filter_width, table + 64) || !splat_lut(table + 64, table, lut, *b0)) return NART_E_INVALID;
+    std::memcpy(cells4, lut.data(), lut.size() * sizeof(float4));
+    *n_cells = (uint32_t)lut.size();
     return NART_OK;
 }
 

@@ -110,3 +110,33 @@ def test_multi_device_create_without_gpu_fails_cleanly(built, glass_scene):
     cnt = C.c_int(-1)
     lib.nart_hip_device_count(C.byref(cnt))
     assert cnt.value == 0
+
+
+def test_splat_weight_cells_reproduce_filter_weight(built):
+    """The splat's weight-by-d2-cell table (nart_hip_splat_lut, k_splat_col4): for every d2 a hit can
+    have, table[AddSample's filter index] (render.cpp:43-50) equals the cell lookup
+    w = d2 >= t ? w_hi : w_lo with cell = clamp((bits(d2) >> 16) - b0, 0, n - 1)."""
+    import numpy as np
+    lib = nart_amd.api.hip_lib()
+    table = nart_amd.filter_table()
+    rng = np.random.default_rng(11)
+    for fw in (2.0, 1.5, 0.5, 1.0, 3.0, 0.75):
+        cells = np.zeros((2048, 4), np.float32)
+        n, b0 = ctypes.c_uint32(), ctypes.c_uint32()
+        assert lib.nart_hip_splat_lut(ctypes.c_float(fw), cells.ctypes.data, ctypes.byref(n), ctypes.byref(b0)) == 0
+        cells = cells[:n.value]
+        thr = np.zeros(65, np.float32)
+        lib.nart_hip_splat_thresholds(ctypes.c_float(fw), thr.ctypes.data)
+        hmax = np.float32(fw + 0.5)
+        d2max = np.float32(2) * hmax * hmax
+        edges = ((np.arange(n.value, dtype=np.uint32) + b0.value) << 16).view(np.float32)
+        d2 = np.concatenate([rng.uniform(0, d2max, 400000).astype(np.float32), thr[1:64],
+                             np.nextafter(thr[1:64], np.float32(0)), edges, np.nextafter(edges, np.float32(0)),
+                             np.float32([0.0, 1e-30, d2max])])
+        d2 = d2[np.isfinite(d2) & (d2 <= d2max) & (d2 >= 0)]
+        q = (np.sqrt(d2) / np.float32(fw)).astype(np.float32) * np.float32(64)
+        want = table[np.minimum(63, q.astype(np.int32) & 0xFF)]
+        c = np.clip((d2.view(np.uint32) >> 16).astype(np.int64) - b0.value, 0, n.value - 1)
+        e = cells[c]
+        got = np.where(d2 >= e[:, 0], e[:, 2], e[:, 1])
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), fw
