@@ -281,7 +281,8 @@ NHD float glibc_atan2f(float y, float x) {
 // glibc 2.35 logf (sysdeps/ieee754/flt-32/e_logf.c, table e_logf_data.c, 16 intervals), in
 // the form x86-64 glibc runs on FMA/AVX2 hosts (the __logf_fma ifunc: the double-precision
 // steps contracted to fused multiply-adds).  SampleExponentialDecay (sampling.cpp:60-62).
-NHD float glibc_logf(float x) {
+// glibc's 16 (invc, logc) pairs, entry i selected without a memory table
+NHD void logf_table(int i, double& invc, double& logc) {
     struct LogfT { double invc, logc; };
     const LogfT T[16] = {
         {0x1.661ec79f8f3bep+0, -0x1.57bf7808caadep-2}, {0x1.571ed4aaf883dp+0, -0x1.2bef0a7c06ddbp-2},
@@ -292,6 +293,18 @@ NHD float glibc_logf(float x) {
         {0x1.e608cfd9a47acp-1, 0x1.aa5aa5df25984p-5},  {0x1.ca4b31f026aap-1, 0x1.c5e53aa362eb4p-4},
         {0x1.b2036576afce6p-1, 0x1.526e57720db08p-3},  {0x1.9c2d163a1aa2dp-1, 0x1.bc2860d22477p-3},
         {0x1.886e6037841edp-1, 0x1.1058bc8a07ee1p-2},  {0x1.767dcf5534862p-1, 0x1.4043057b6ee09p-2}};
+    invc = i == 0 ? T[0].invc : 0.0;
+    logc = i == 0 ? T[0].logc : 0.0;
+#pragma unroll
+    for (int j = 1; j < 16; ++j)
+        if (i == j) {
+            invc = T[j].invc;
+            logc = T[j].logc;
+        }
+}
+// logf with the table entry supplied by lookup(i, invc, logc)
+template <typename Lookup>
+NHD float glibc_logf_with(float x, Lookup lookup) {
     const double Ln2 = 0x1.62e42fefa39efp-1, A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2,
                  A2 = -0x1.ffffef20a4123p-2;
     uint32_t ix = ubits(x);
@@ -307,13 +320,8 @@ NHD float glibc_logf(float x) {
     const int i = (int)((tmp >> 19) % 16);
     const int k = (int32_t)tmp >> 23;
     const uint32_t iz = ix - (tmp & 0xff800000u);
-    double invc = i == 0 ? T[0].invc : 0.0, logc = i == 0 ? T[0].logc : 0.0;
-#pragma unroll
-    for (int j = 1; j < 16; ++j)
-        if (i == j) {
-            invc = T[j].invc;
-            logc = T[j].logc;
-        }
+    double invc, logc;
+    lookup(i, invc, logc);
     const double z = (double)fbits(iz);
     const double r = __builtin_fma(z, invc, -1.0);
     const double y0 = __builtin_fma((double)k, Ln2, logc);
@@ -322,6 +330,9 @@ NHD float glibc_logf(float x) {
     y = __builtin_fma(r2, A0, y);
     y = __builtin_fma(r2, y, r + y0);
     return (float)y;
+}
+NHD float glibc_logf(float x) {
+    return glibc_logf_with(x, [](int i, double& invc, double& logc) { logf_table(i, invc, logc); });
 }
 
 ND float rng_float(uint32_t& y) {

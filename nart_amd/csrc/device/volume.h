@@ -247,12 +247,20 @@ template <bool COUNT>
 __global__ __launch_bounds__(256) void k_render_volume_sm(DScene S, RenderArgs A) {
     // A.lds_nodes != 0: the density grid (that many floats) is staged in LDS
     extern __shared__ float s_dens[];
+    // glibc logf's (invc, logc) table: one LDS read per tentative collision instead of a
+    // 16-way select of double pairs (~80 VALU instructions)
+    __shared__ double2 s_logf[16];
+    if (threadIdx.x < 16) {
+        double invc, logc;
+        logf_table((int)threadIdx.x, invc, logc);
+        s_logf[threadIdx.x] = make_double2(invc, logc);
+    }
     DMedium mloc = S.medium;
     if (A.lds_nodes) {
         for (uint32_t i = threadIdx.x; i < A.lds_nodes; i += blockDim.x) s_dens[i] = S.medium.density[i];
-        __syncthreads();
         mloc.density = s_dens;
     }
+    __syncthreads();
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= A.n_slots) return;
     const uint32_t slot = A.queue ? A.queue[gid] : gid;
@@ -304,7 +312,11 @@ __global__ __launch_bounds__(256) void k_render_volume_sm(DScene S, RenderArgs A
         }
         if (ph == P_COLL) {
             ++work;
-            const float t = tMin + (-glibc_logf(1.f - rng_float(rng)) / sigma);
+            const float t = tMin + (-glibc_logf_with(1.f - rng_float(rng), [&](int i, double& invc, double& logc) {
+                                         const double2 e = s_logf[i];
+                                         invc = e.x;
+                                         logc = e.y;
+                                     }) / sigma);
             if (!(t < t1)) {
                 ph = P_MAJ;
             } else {

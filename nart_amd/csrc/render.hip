@@ -288,7 +288,8 @@ int check_params(nart_ctx* ctx, const nart_render_params* p) {
 // MI355X holds 288 GB, so by default a batch may take half of the device memory free at the call
 // (plus what this context already holds for it), at least 16 GiB: whole frames up to 4K x 512 spp
 // (119 GB) render in one batch -- fewer launch tails than the former fixed 16 GiB (C5 469 -> 413
-// ms, C4 5.27 -> 4.43 s per frame; profiles/r03a_batch_ab.log).  NART_BATCH_BYTES overrides.
+// ms, C4 5.27 -> 4.43 s per frame; profiles/r03a_bb_c4.log, r03a_bb_c5_s*.log).  NART_BATCH_BYTES
+// overrides.
 size_t batch_slot_limit(const nart_ctx* ctx, uint32_t spp) {
     size_t budget = (size_t)16 << 30;
     size_t free_b = 0, total_b = 0;
