@@ -288,6 +288,161 @@ __global__ __launch_bounds__(64) void k_latin_idx(RenderArgs A, float* scratch) 
     const_cast<uint32_t*>(A.rng0)[slot] = rng;
 }
 
+// ---------------------------------------------------------------- LatinSquare in three kernels
+// The shuffle's transpositions (i, c_i) depend only on the pixel's RNG stream, never on the
+// values being shuffled (sampling.cpp:80-85), and a jittered stratum value depends only on the
+// stream position that drew it (sampling.cpp:64-67, 75-78).  So the serial RNG work leaves the
+// LDS-bound kernel, and the values are never gathered at random from HBM:
+//  k_latin_draws  lane per slot, no LDS (full occupancy): runs the pixel's 2n generation draws,
+//                 recording the state after each x draw (st[k] = state after draw 2k+1), then the
+//                 2n shuffle choices c_x(i), c_y(i), and writes the final state (rng0);
+//  k_latin_perm   lane per slot, u16 stratum indices in LDS ([i][lane]): replays the swaps, x then
+//                 y, with the choices streamed from HBM; writes the final index arrays;
+//  k_latin_emit   16 slots per block, their st[] staged in LDS: sample j gets
+//                 (val_x(sx[j]), val_y(sy[j])) with val_x(k) from st[k] and val_y(k) from one
+//                 more xorshift step.
+// Scratch (in Lout, which the path kernel overwrites later): cx, cy, sx, sy are u16 pairs in u32
+// words [slot / 64][i / 2][slot % 64] (low half = even i); st is u32 [slot / 16][k][slot % 16].
+struct LatinScratch {
+    uint32_t *cx, *cy, *sx, *sy, *st;
+    uint32_t n2;  // (spp + 1) / 2 word rows
+};
+#define LATIN_EMIT_SLOTS 16
+
+ND size_t latin_row(uint32_t g, uint32_t rows, uint32_t r, uint32_t lane) {
+    return ((size_t)g * rows + r) * 64u + lane;
+}
+
+__global__ __launch_bounds__(256) void k_latin_draws(RenderArgs A, LatinScratch L) {
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot >= A.n_slots) return;
+    const uint32_t g = slot >> 6, lane = slot & 63u, n = A.spp;
+    const uint32_t xy = A.slot_xy[slot];
+    uint32_t rng = ((xy >> 16) * A.totalW + (xy & 0xFFFFu)) + 2463534242u;  // RNG::Seed (rng.h:10-13)
+    // generation: x of stratum k is draw 2k+1, y draw 2k+2 (Q2)
+    uint32_t* st = L.st + (size_t)(slot / LATIN_EMIT_SLOTS) * n * LATIN_EMIT_SLOTS + slot % LATIN_EMIT_SLOTS;
+    for (uint32_t k = 0; k < n; ++k) {
+        rng = xorshift(rng);
+        st[(size_t)k * LATIN_EMIT_SLOTS] = rng;
+        rng = xorshift(rng);
+    }
+    for (uint32_t i2 = 0; i2 < L.n2; ++i2) {
+        uint32_t wx = 0, wy = 0;
+        for (uint32_t h = 0; h < 2; ++h) {
+            const uint32_t i = 2 * i2 + h;
+            if (i >= n) break;
+            wx |= rng_int(rng, n - 1 - i) << (16 * h);  // sampling.cpp:81-84, x choice first
+            wy |= rng_int(rng, n - 1 - i) << (16 * h);
+        }
+        L.cx[latin_row(g, L.n2, i2, lane)] = wx;
+        L.cy[latin_row(g, L.n2, i2, lane)] = wy;
+    }
+    const_cast<uint32_t*>(A.rng0)[slot] = rng;
+}
+
+#ifndef NART_LATIN_PF
+#define NART_LATIN_PF 16  // choice words (2 swaps each) loaded one batch ahead of their swaps
+#endif
+__global__ __launch_bounds__(64) void k_latin_perm(RenderArgs A, LatinScratch L) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t s_idx[];
+    const uint32_t lane = threadIdx.x, g = blockIdx.x;
+    if (g * 64u + lane >= A.n_slots) return;
+    const uint32_t n = A.spp, n2 = L.n2;
+    uint16_t* ix = s_idx + lane;
+    for (int pass = 0; pass < 2; ++pass) {
+        const uint32_t* c = (pass ? L.cy : L.cx) + latin_row(g, n2, 0, lane);
+        uint32_t* so = (pass ? L.sy : L.sx) + latin_row(g, n2, 0, lane);
+        // rolling prefetch: the next PF choice words load while the current PF words' swaps run
+        // (a batch that waits for its own loads stalls on the full HBM latency every 2*PF swaps)
+        constexpr uint32_t PF = NART_LATIN_PF;
+        uint32_t cur[PF], nxt[PF];
+#pragma unroll
+        for (uint32_t u = 0; u < PF; ++u) cur[u] = u < n2 ? c[(size_t)u * 64] : 0u;
+        for (uint32_t i = 0; i < 2 * n2; ++i) ix[i * 64] = (uint16_t)i;
+        for (uint32_t i2 = 0; i2 < n2; i2 += PF) {
+#pragma unroll
+            for (uint32_t u = 0; u < PF; ++u) nxt[u] = i2 + PF + u < n2 ? c[(size_t)(i2 + PF + u) * 64] : 0u;
+#pragma unroll
+            for (uint32_t u = 0; u < PF; ++u) {
+#pragma unroll
+                for (uint32_t h = 0; h < 2; ++h) {
+                    const uint32_t i = 2 * (i2 + u) + h;
+                    if (i < n) {
+                        const uint32_t ci = (cur[u] >> (16 * h)) & 0xFFFFu;
+                        const uint16_t t = ix[i * 64];
+                        ix[i * 64] = ix[ci * 64];
+                        ix[ci * 64] = t;
+                    }
+                }
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < PF; ++u) cur[u] = nxt[u];
+        }
+        for (uint32_t j2 = 0; j2 < n2; ++j2)
+            so[(size_t)j2 * 64] = (uint32_t)ix[2 * j2 * 64] | ((uint32_t)ix[(2 * j2 + 1) * 64] << 16);
+    }
+}
+
+// StratifiedSample1D (sampling.cpp:64-67) from the RNG state its UniformFloat ended in
+ND float latin_value(uint32_t k, uint32_t y, float inv) {
+    const float f = gmin(ND_ONE_MINUS_EPS, (float)(uint32_t)(y * 0x9E3779BBu) * 2.3283064365386963e-10f);
+    return ((float)k + f) * inv;
+}
+
+// Thread t of a block: slot p = t % 16 of the block's 16, sample rows j2 = t / 16 + 16 i, so a
+// wave writes 4 rows x 16 neighbouring slots (128 B each in the bucket layout).  The index words
+// are loaded LATIN_EMIT_U rows ahead (the first batch before the LDS staging): with 2 blocks per
+// CU the kernel is otherwise bound by waiting on them.
+#ifndef LATIN_EMIT_U
+#define LATIN_EMIT_U 8
+#endif
+__global__ __launch_bounds__(256) void k_latin_emit(RenderArgs A, LatinScratch L) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_st[];  // [k][p]
+    constexpr uint32_t P = LATIN_EMIT_SLOTS, RS = 256 / P, U = LATIN_EMIT_U;
+    const uint32_t n = A.spp, n2 = L.n2, t = threadIdx.x, p = t % P;
+    const uint32_t slot = blockIdx.x * P + p;
+    const bool live = slot < A.n_slots;
+    const uint32_t* sx = L.sx + latin_row(slot >> 6, n2, 0, slot & 63u);
+    const uint32_t* sy = L.sy + latin_row(slot >> 6, n2, 0, slot & 63u);
+    uint32_t cx[U], cy[U], nx[U], ny[U];
+    const uint32_t j0 = t / P;
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+        const uint32_t j2 = j0 + u * RS;
+        cx[u] = live && j2 < n2 ? sx[(size_t)j2 * 64] : 0u;
+        cy[u] = live && j2 < n2 ? sy[(size_t)j2 * 64] : 0u;
+    }
+    const uint32_t* stg = L.st + (size_t)blockIdx.x * n * P;
+    for (uint32_t i = t; i < n * P; i += blockDim.x) s_st[i] = stg[i];
+    __syncthreads();
+    if (!live) return;
+    const float inv = 1.f / (float)n;
+    const SlotSO so = A.slot_so[slot];
+    float2* s = const_cast<float2*>(A.samples) + so.first;
+    for (uint32_t jb = j0; jb < n2; jb += U * RS) {
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t j2 = jb + (U + u) * RS;
+            nx[u] = j2 < n2 ? sx[(size_t)j2 * 64] : 0u;
+            ny[u] = j2 < n2 ? sy[(size_t)j2 * 64] : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+#pragma unroll
+            for (uint32_t h = 0; h < 2; ++h) {
+                const uint32_t j = 2 * (jb + u * RS) + h;
+                if (j < n) {
+                    const uint32_t kx = (cx[u] >> (16 * h)) & 0xFFFFu, ky = (cy[u] >> (16 * h)) & 0xFFFFu;
+                    s[(size_t)j * so.stride] = make_float2(latin_value(kx, s_st[kx * P + p], inv),
+                                                           latin_value(ky, xorshift(s_st[ky * P + p]), inv));
+                }
+            }
+            cx[u] = nx[u];
+            cy[u] = ny[u];
+        }
+    }
+}
+
 enum { ST_EXT = 0, ST_SH1 = 1, ST_SH2 = 2 };
 
 // ---------------------------------------------------------------- path tracing megakernel
@@ -1821,6 +1976,239 @@ __global__ __launch_bounds__(256) void k_splat_col4(SplatArgs A) {
         o[3] = czw[j].y;
         o[4] = cws[j];
     }
+}
+
+// Skewed-time splat over the pixel-major sample layout (sample i of bucket-local pixel q at
+// (base + q) * spp + i), one lane per tile column, LUT filter weights (power-of-two buckets).
+// AddSample (render.cpp:23-70) adds a bucket's sources to the tile in raster order; a tile pixel
+// (tx, ty) receives sources (sy, sx) with sy in [ty-2R, ty], sx in [tx-2R, tx] (R = filterBounds),
+// i.e. in increasing step t = W sy + sx (W = 2R + 1 > the window's column span).  Processing
+// source s at step t(s) for all its consumers at once therefore keeps every tile pixel's order,
+// and at step t lane tx has exactly one candidate source: the sx in [tx-2R, tx] with
+// sx = t (mod W), sy = (t - sx) / W, which it adds to its W window rows [sy, sy+2R] (registers;
+// a row is written out once its last source row is done).  The W lanes tx in [sx, sx+2R] read
+// source s at the same step, so each sample is fetched once per bucket (k_splat_col4 fetches it
+// ~12 times through L2), and each loaded sample serves W tile pixels of the lane.
+// Bucket-edge wraps (a last-column / last-row sample whose coordinate rounds onto the next
+// bucket's origin: splat_hits) go to tile columns / rows 0..2R+1 at their raster position: a
+// pre-pass flags the edge sources that have such samples, and only flagged sources get the
+// extra passes (the x wrap: source (sy, B-1) after the lane's last source of row sy, as the
+// gather kernels' extra column; the y wrap: the already written rows 0..2R+1, read back and
+// updated at source row B-1).  Per pair the arithmetic is splat_hits_fast + the LUT weight, as
+// in k_splat_col4: bit-identical.
+template <int R>
+__global__ __launch_bounds__(256) void k_splat_skew(SplatArgs A) {
+    constexpr int W = 2 * R + 1, NWR = 2 * R + 2;
+    extern __shared__ __attribute__((aligned(16))) float4 s_dyn4[];
+    float4* s_lut = s_dyn4;
+    uint32_t* s_flag = reinterpret_cast<uint32_t*>(s_dyn4 + A.lut_n);  // [bucket of block][x, y]
+    const uint32_t T = A.tile, PB = 64u / T, wv = threadIdx.x >> 6, l = threadIdx.x & 63u;
+    for (uint32_t i = threadIdx.x; i < A.lut_n; i += blockDim.x) s_lut[i] = A.lut[i];
+    if (threadIdx.x < 8u * PB) s_flag[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint32_t lb = l / T, tx = l % T;
+    const uint32_t bi = (blockIdx.x * 4u + wv) * PB + lb;
+    const bool live = lb < PB && bi < A.n_buckets;
+    uint32_t* flag = s_flag + 2u * (wv * PB + (lb < PB ? lb : 0u));
+    uint32_t bid = 0, x0 = 0, y0 = 0, base = 0;
+    int bw = 0, bh = 0;
+    const int B = (int)A.B;
+    if (live) {
+        bid = A.bucket_ids[bi];
+        x0 = A.B * (bid % A.nbx);
+        y0 = A.B * (bid / A.nbx);
+        bw = (int)(min(x0 + A.B, A.totalW) - x0);
+        bh = (int)(min(y0 + A.B, A.totalH) - y0);
+        base = A.bucket_base[bi];
+    }
+    const float fw = A.fw, fbf = (float)A.fb;
+    const float edgeX = (float)(x0 + A.B + A.fb), edgeY = (float)(y0 + A.B + A.fb);
+    // pre-pass: which last-column sources (bit sy) / last-row sources (bit sx) have wrapping samples
+    if (live) {
+        for (int k = (int)tx; k < 2 * B; k += (int)T) {
+            const bool colsrc = k < B;
+            const int sy = colsrc ? k : B - 1, sx = colsrc ? B - 1 : k - B;
+            if ((colsrc && bw != B) || (!colsrc && bh != B) || sy >= bh || sx >= bw) continue;
+            const float2* sp = A.samples + (size_t)(base + (uint32_t)(sy * bw + sx)) * A.spp;
+            const float f = colsrc ? (float)(x0 + (uint32_t)sx + A.fb) : (float)(y0 + (uint32_t)sy + A.fb);
+            const float edge = colsrc ? edgeX : edgeY;
+            bool any = false;
+            for (uint32_t i = 0; i < A.spp && !any; ++i) {
+                const float2 u = sp[i];
+                any = (f + (colsrc ? u.x : u.y)) >= edge;
+            }
+            if (any) atomicOr(flag + (colsrc ? 0 : 1), 1u << (colsrc ? sy : sx));
+        }
+    }
+    __syncthreads();
+    if (!live) return;
+    const uint32_t flagX = flag[0], flagY = flag[1];
+    const float xsA = (float)(tx + x0), xsB = (float)(tx + x0 + A.B);
+    const int lut_b0 = (int)A.lut_b0, lut_last = (int)A.lut_n - 1;
+    nd_f2v cxy[W], czw[W];
+    float cws[W];
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        cxy[k] = nd_f2v{0.f, 0.f};
+        czw[k] = nd_f2v{0.f, 0.f};
+        cws[k] = 0.f;
+    }
+    int wb = 0;  // tile row of cxy[0]
+    const uint32_t tpx = T * T;
+    float* out = A.tiles + ((uint64_t)bi * tpx + tx) * 5;  // + ty * T * 5
+    auto retire = [&]() {
+        float* o = out + (size_t)wb * T * 5;
+        o[0] = cxy[0].x;
+        o[1] = cxy[0].y;
+        o[2] = czw[0].x;
+        o[3] = czw[0].y;
+        o[4] = cws[0];
+#pragma unroll
+        for (int k = 0; k + 1 < W; ++k) {
+            cxy[k] = cxy[k + 1];
+            czw[k] = czw[k + 1];
+            cws[k] = cws[k + 1];
+        }
+        cxy[W - 1] = nd_f2v{0.f, 0.f};
+        czw[W - 1] = nd_f2v{0.f, 0.f};
+        cws[W - 1] = 0.f;
+        ++wb;
+    };
+    float fy = 0.f, ybA = 0.f, ybB = 0.f;  // per source row: fy, and the window's first image row
+                                           // without / with the y wrap (splat_hits_fast)
+    float fx = 0.f;
+    // one sample into the window rows wb .. wb+2R
+    auto splat_w = [&](float2 uv, float4 L) {
+        const float scx = fx + uv.x, scy = fy + uv.y;
+        const float xs = scx >= edgeX ? xsB : xsA;
+        const bool xhit = (scx - fw) < xs + 1.f && xs < (scx + fw);
+        const float distX = (xs + 0.5f) - scx;
+        const float dx2 = distX * distX;
+        const float yb = scy >= edgeY ? ybB : ybA;
+        const float loy = scy - fw, hiy = scy + fw;
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+            const float ys = yb + (float)k;
+            const bool hit = xhit && loy < ys + 1.f && ys < hiy;
+            const float distY = (ys + 0.5f) - scy;
+            const float d2 = dx2 + distY * distY;
+            int cell = (int)(__float_as_uint(d2) >> 16) - lut_b0;
+            cell = cell < 0 ? 0 : (cell > lut_last ? lut_last : cell);
+            const float4 e = s_lut[cell];
+            const float w = d2 >= e.x ? e.z : e.y;
+            if (hit) {
+                const nd_f2v w2 = nd_f2v{w, w};
+                cxy[k] += nd_f2v{L.x, L.y} * w2;
+                czw[k] += nd_f2v{L.z, L.w} * w2;
+                cws[k] += w;
+            }
+        }
+    };
+    auto source_pass = [&](int sy, int sx) {  // every sample of bucket-local pixel (sx, sy)
+        const size_t first = (size_t)(base + (uint32_t)(sy * bw + sx)) * A.spp;
+        const float2* sp = A.samples + first;
+        const float4* lp = A.Lout + first;
+        fx = (float)(x0 + (uint32_t)sx + A.fb);
+        constexpr uint32_t PF = 4;
+        uint32_t i = 0;
+        float2 nu[PF];
+        float4 nL[PF];
+        if (A.spp >= PF) {
+#pragma unroll
+            for (uint32_t u = 0; u < PF; ++u) {
+                nu[u] = sp[u];
+                nL[u] = lp[u];
+            }
+        }
+        for (; i + PF <= A.spp; i += PF) {
+            float2 uv[PF];
+            float4 Lv[PF];
+#pragma unroll
+            for (uint32_t u = 0; u < PF; ++u) {
+                uv[u] = nu[u];
+                Lv[u] = nL[u];
+            }
+            if (i + 2 * PF <= A.spp) {
+#pragma unroll
+                for (uint32_t u = 0; u < PF; ++u) {
+                    nu[u] = sp[i + PF + u];
+                    nL[u] = lp[i + PF + u];
+                }
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < PF; ++u) splat_w(uv[u], Lv[u]);
+        }
+        for (; i < A.spp; ++i) splat_w(sp[i], lp[i]);
+    };
+    // y wrap (rare): samples of last-row source (B-1, sx) at or past edgeY into the written
+    // tile rows 0 .. min(2R+1, B-2) of this lane's column, read back from the tile output
+    auto ywrap_pass = [&](int sx) {
+        const int sy = B - 1;
+        const size_t first = (size_t)(base + (uint32_t)(sy * bw + sx)) * A.spp;
+        const float2* sp = A.samples + first;
+        const float4* lp = A.Lout + first;
+        const float fxw = (float)(x0 + (uint32_t)sx + A.fb), fyw = (float)(y0 + (uint32_t)sy + A.fb);
+        const int nr = min(NWR, B - 1);
+        float acc[NWR][5];
+#pragma unroll
+        for (int k = 0; k < NWR; ++k)
+#pragma unroll
+            for (int c = 0; c < 5; ++c) acc[k][c] = k < nr ? out[(size_t)k * T * 5 + c] : 0.f;
+        const float ysB0 = (float)(y0 + A.B);
+        for (uint32_t i = 0; i < A.spp; ++i) {
+            const float2 uv = sp[i];
+            const float scx = fxw + uv.x, scy = fyw + uv.y;
+            if (!(scy >= edgeY)) continue;
+            const float4 L = lp[i];
+            const float xs = scx >= edgeX ? xsB : xsA;
+            const bool xhit = (scx - fw) < xs + 1.f && xs < (scx + fw);
+            const float distX = (xs + 0.5f) - scx;
+            const float dx2 = distX * distX;
+            const float loy = scy - fw, hiy = scy + fw;
+#pragma unroll
+            for (int k = 0; k < NWR; ++k) {
+                const float ys = ysB0 + (float)k;
+                const bool hit = k < nr && xhit && loy < ys + 1.f && ys < hiy;
+                const float distY = (ys + 0.5f) - scy;
+                const float d2 = dx2 + distY * distY;
+                int cell = (int)(__float_as_uint(d2) >> 16) - lut_b0;
+                cell = cell < 0 ? 0 : (cell > lut_last ? lut_last : cell);
+                const float4 e = s_lut[cell];
+                const float w = d2 >= e.x ? e.z : e.y;
+                if (hit) {
+                    acc[k][0] += L.x * w;
+                    acc[k][1] += L.y * w;
+                    acc[k][2] += L.z * w;
+                    acc[k][3] += L.w * w;
+                    acc[k][4] += w;
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NWR; ++k)
+            if (k < nr)
+#pragma unroll
+                for (int c = 0; c < 5; ++c) out[(size_t)k * T * 5 + c] = acc[k][c];
+    };
+    const bool xwrap_lane = bw == B && (int)tx <= 2 * R + 1 && bw - 1 > (int)tx;
+    const int tmax = W * (B - 1) + (B - 1);
+    for (int t = 0; t <= tmax; ++t) {
+        const int d = (((int)tx - t) % W + W) % W;
+        const int sx = (int)tx - d, sy = (t - sx) / W;
+        if (sx < 0 || sx >= bw || sy < 0 || sy >= bh) continue;
+        while (wb < sy) retire();
+        fy = (float)(y0 + (uint32_t)sy + A.fb);
+        ybA = (float)(y0 + (uint32_t)sy);
+        ybB = (float)(y0 + A.B + (uint32_t)sy);
+        source_pass(sy, sx);
+        const bool ylast = bh == B && sy == B - 1;
+        if (ylast && ((flagY >> sx) & 1u)) ywrap_pass(sx);
+        if (xwrap_lane && sx == (int)tx && ((flagX >> sy) & 1u)) {  // the gather kernels' extra column
+            source_pass(sy, bw - 1);
+            if (ylast && ((flagY >> (bw - 1)) & 1u)) ywrap_pass(bw - 1);
+        }
+    }
+    while (wb < (int)T) retire();
 }
 
 // ---------------------------------------------------------------- combine

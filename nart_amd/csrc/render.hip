@@ -30,7 +30,7 @@ struct nart_ctx {
     uint32_t num_nodes = 0;
     int variant = 0;
     // 3 four pixels per lane (default), 2/1/0 one pixel per lane
-    int splat_mode = 3;
+    int splat_mode = 4;
     bool counters = false;
     bool has_env = false;  // scene has an environment light (selects the k_render build)
     // scene buffers
@@ -482,12 +482,16 @@ __global__ void k_build_queue(const uint32_t* top, const uint32_t* rest, uint32_
 int sort_groups_by_cost(nart_ctx* ctx, uint32_t n, uint32_t* out, hipStream_t st);
 
 // Sample-major bucket layout: slot `base + p` of a bucket of `cnt` traced pixels keeps sample s
-// at base*spp + s*cnt + p.  One block per bucket of the batch.
-__global__ void k_slot_table(const uint32_t* bucket_base, uint32_t nbk, uint32_t nslots, uint32_t spp, SlotSO* so) {
+// at base*spp + s*cnt + p (k_splat_col4's lanes then read neighbouring pixels' sample s from one
+// line); pixel-major: at (base + p)*spp + s (k_splat_skew streams one pixel's samples).  One
+// block per bucket of the batch.
+__global__ void k_slot_table(const uint32_t* bucket_base, uint32_t nbk, uint32_t nslots, uint32_t spp, SlotSO* so,
+                             bool pixel_major) {
     const uint32_t b = blockIdx.x;
     const uint32_t base = bucket_base[b], end = b + 1 < nbk ? bucket_base[b + 1] : nslots;
     for (uint32_t p = threadIdx.x; base + p < end; p += blockDim.x)
-        so[base + p] = SlotSO{(unsigned long long)base * spp + p, end - base, 0u};
+        so[base + p] = pixel_major ? SlotSO{(unsigned long long)(base + p) * spp, 1u, 0u}
+                                   : SlotSO{(unsigned long long)base * spp + p, end - base, 0u};
 }
 
 __global__ void k_slot_rows(uint32_t n, uint32_t spp, SlotSO* so) {
@@ -869,6 +873,29 @@ bool splat_lut(const float thr[65], const float table[64], std::vector<float4>& 
 // spp (scratch in Lout: 2*spp floats per lane of every launched block, within Lout's 4*spp per
 // slot once there are >= 64 slots), the global-memory variant beyond.
 int launch_latin(nart_ctx* ctx, const RenderArgs& ra, hipStream_t st) {
+    // three-kernel form (k_latin_draws / _perm / _emit) when its scratch fits in Lout
+    static const int latin_env = std::getenv("NART_LATIN") ? std::atoi(std::getenv("NART_LATIN")) : -1;
+    const uint32_t groups = (ra.n_slots + 63) / 64;
+    LatinScratch ls;
+    ls.n2 = (ra.spp + 1) / 2;
+    const size_t words = (size_t)groups * 64 * ls.n2;
+    const size_t stw = (size_t)((ra.n_slots + LATIN_EMIT_SLOTS - 1) / LATIN_EMIT_SLOTS) * LATIN_EMIT_SLOTS * ra.spp;
+    const bool three = ra.spp >= 2 && ra.spp <= 1024 && (4 * words + stw) * 4 <= ctx->cap_samples * sizeof(float4) &&
+                       (latin_env == 3 || (latin_env < 0 && ra.spp > 256));
+    if (three) {
+        uint32_t* base = reinterpret_cast<uint32_t*>(ra.Lout);
+        ls.cx = base;
+        ls.cy = base + words;
+        ls.sx = base + 2 * words;
+        ls.sy = base + 3 * words;
+        ls.st = base + 4 * words;
+        hipLaunchKernelGGL(k_latin_draws, dim3((ra.n_slots + 255) / 256), dim3(256), 0, st, ra, ls);
+        hipLaunchKernelGGL(k_latin_perm, dim3(groups), dim3(64), (size_t)ls.n2 * 2 * 64 * sizeof(uint16_t), st, ra, ls);
+        hipLaunchKernelGGL(k_latin_emit, dim3((ra.n_slots + LATIN_EMIT_SLOTS - 1) / LATIN_EMIT_SLOTS), dim3(256),
+                           (size_t)ra.spp * LATIN_EMIT_SLOTS * sizeof(uint32_t), st, ra, ls);
+        HIPCHK(hipGetLastError());
+        return NART_OK;
+    }
     // (k_latin_idx at <= 256 spp measured slower: C3 11.0 vs 6.6 ms)
     if (ra.spp <= 256) {
         size_t lds = (size_t)ra.spp * 2 * 64 * sizeof(float);
@@ -904,6 +931,11 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
     uint32_t lut_b0 = 0;
     static const bool lut_env = !(std::getenv("NART_SPLAT_LUT") && std::getenv("NART_SPLAT_LUT")[0] == '0');
     const bool lut_ok = lut_env && thr_ok && splat_lut(table + 64, table, lut, lut_b0);
+    // skewed-time splat (k_splat_skew, pixel-major samples) where its preconditions hold, else
+    // k_splat_col4 / k_splat over the sample-major layout
+    const uint32_t B = p->bucket_size, tile = B + 2 * g.filter_bounds;
+    const bool skew = ctx->splat_mode >= 4 && lut_ok && (B & (B - 1)) == 0 && B <= 32 && tile <= 64 &&
+                      g.filter_bounds >= 1 && g.filter_bounds <= 3;
     if (lut_ok) {
         if (!ctx->d_lut) HIPCHK(hipMalloc(&ctx->d_lut, SPLAT_LUT_MAX * sizeof(float4)));
         HIPCHK(hipMemcpy(ctx->d_lut, lut.data(), lut.size() * sizeof(float4), hipMemcpyHostToDevice));
@@ -955,7 +987,7 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         HIPCHK(hipMemcpyAsync(ctx->d_bucket_ids, ids + b0, (size_t)nbk * 4, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(ctx->d_bucket_base, base.data(), (size_t)nbk * 4, hipMemcpyHostToDevice, st));
         hipLaunchKernelGGL(k_slot_table, dim3(nbk), dim3(256), 0, st, ctx->d_bucket_base, nbk, nslots, p->spp,
-                           ctx->d_slot_so);
+                           ctx->d_slot_so, skew);
         RenderArgs ra;
         ra.slot_xy = ctx->d_slot_xy;
         ra.slot_so = ctx->d_slot_so;
@@ -1016,7 +1048,13 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         const uint64_t n4 = (uint64_t)nbk * g.tile_size * ((g.tile_size + NART_SPLAT_NP - 1) / NART_SPLAT_NP);
         // splat modes (all bit-identical, mode 3 the default): 3 four tile pixels per lane; 2 / 1 / 0
         // one tile pixel per lane with the compare-only / threshold / direct filter-index arithmetic
-        if (sa.thr && sa.invB != 0.f && splat_mode >= 3)
+        if (skew) {
+            const uint32_t pb = 64u / g.tile_size, nblk = (nbk + 4 * pb - 1) / (4 * pb);
+            const size_t lds = lut.size() * sizeof(float4) + 8u * pb * sizeof(uint32_t);
+            if (g.filter_bounds == 1) hipLaunchKernelGGL(k_splat_skew<1>, dim3(nblk), dim3(256), lds, st, sa);
+            else if (g.filter_bounds == 2) hipLaunchKernelGGL(k_splat_skew<2>, dim3(nblk), dim3(256), lds, st, sa);
+            else hipLaunchKernelGGL(k_splat_skew<3>, dim3(nblk), dim3(256), lds, st, sa);
+        } else if (sa.thr && sa.invB != 0.f && splat_mode >= 3)
         {
             if (sa.lut)
                 hipLaunchKernelGGL((k_splat_col4<NART_SPLAT_NP, true>), dim3((uint32_t)((n4 + 255) / 256)), dim3(256), 0,
@@ -1268,7 +1306,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
         const int var = std::atoi(v);
         if (var == 0 || var == 2 || var == 3) ctx->variant = var;
     }
-    if (const char* v = std::getenv("NART_SPLAT_MODE")) ctx->splat_mode = std::max(0, std::min(3, std::atoi(v)));
+    if (const char* v = std::getenv("NART_SPLAT_MODE")) ctx->splat_mode = std::max(0, std::min(4, std::atoi(v)));
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device_id || device_id < 0) {
         delete ctx;
@@ -1286,6 +1324,11 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
         return bail(NART_E_HIP);
     if (hipFuncSetAttribute((const void*)k_latin_idx, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
         hipSuccess)
+        return bail(NART_E_HIP);
+    if (hipFuncSetAttribute((const void*)k_latin_perm, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+            hipSuccess ||
+        hipFuncSetAttribute((const void*)k_latin_emit, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+            hipSuccess)
         return bail(NART_E_HIP);
     // reference octree visibility (Q14) + device BVH
     std::vector<uint8_t> mask;
@@ -1501,9 +1544,10 @@ int nart_hip_set_splat_mode(nart_ctx* ctx, int mode) {
     if (!ctx) return NART_E_INVALID;
     for (nart_ctx* c : ctx->subs)
         if (int rc = nart_hip_set_splat_mode(c, mode)) return fail(ctx, rc, c->err);
-    if (mode < 0 || mode > 3)
-        return fail(ctx, NART_E_UNSUPPORTED, "splat mode must be 0-3 (3 four pixels per lane, 2-0 one pixel per lane; "
-                                             "the LDS-staged and tile-column-sweep modes were retired, DESIGN.md)");
+    if (mode < 0 || mode > 4)
+        return fail(ctx, NART_E_UNSUPPORTED, "splat mode must be 0-4 (4 skewed-time tile columns, 3 four pixels per "
+                                             "lane, 2-0 one pixel per lane; the LDS-staged and tile-column-sweep modes "
+                                             "were retired, DESIGN.md)");
     ctx->splat_mode = mode;
     return NART_OK;
 }

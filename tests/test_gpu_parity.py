@@ -343,7 +343,7 @@ def test_latin_square_high_spp_frame(gpu, glass_scene, glass_oracle):
 
 
 @pytest.mark.parametrize("bucket,fw", [(12, 2.0), (16, 1.0), (8, 2.5), (10, 0.75), (16, 3.0), (4, 0.25)])
-@pytest.mark.parametrize("splat_mode", [3, 2, 0], ids=["col4", "compare", "direct"])
+@pytest.mark.parametrize("splat_mode", [4, 3, 2, 0], ids=["skew", "col4", "compare", "direct"])
 def test_splat_bucket_and_filter_sizes(gpu, glass_scene, glass_oracle, bucket, fw, splat_mode):
     """Splat arithmetic paths: power-of-two buckets use the compare-only pair test, other sizes
     the direct one; filter widths with threshold-derived indices (fw > ~0.28) and without (0.25);
@@ -352,6 +352,53 @@ def test_splat_bucket_and_filter_sizes(gpu, glass_scene, glass_oracle, bucket, f
     g = nart_amd.HipRenderer(glass_scene, splat_mode=splat_mode).render(p)
     o = glass_oracle.render(p)
     assert _bits_equal(g, o), _report(g, o)
+
+
+def _edge_wrap_buckets(p, n_each=2):
+    """Full buckets of a wide frame whose last-column / last-row samples round onto the next
+    bucket's origin (render.cpp:52-61: splatted through glm::mod into the start of their own
+    tile).  Far from the origin a float32 coordinate's spacing is 2^-8, so the last stratum's
+    u rounds up often.  Returns bucket ids: x-wrap only, y-wrap only, and the corner pixel both."""
+    g = nart_amd.session_geometry(p)
+    B, fb = p.bucket_size, g.filter_bounds
+
+    def wraps(x, y, axis):
+        uv, _ = oracle.latin_square(y * g.total_width + x, p.spp)
+        c = (x if axis == 0 else y) + fb
+        return bool((np.float32(c) + uv[:, axis] >= np.float32(c + 1)).any())
+
+    xs, ys, corner = [], [], []
+    for by in range(g.n_buckets_y - 2, 0, -1):
+        for bx in range(g.n_buckets_x - 2, g.n_buckets_x - 40, -1):
+            x0, y0 = bx * B, by * B
+            cx, cy = wraps(x0 + B - 1, y0 + B - 1, 0), wraps(x0 + B - 1, y0 + B - 1, 1)
+            if cx and cy and len(corner) < 1:
+                corner.append(by * g.n_buckets_x + bx)
+            elif len(xs) < n_each and any(wraps(x0 + B - 1, y0 + j, 0) for j in range(B - 1)):
+                xs.append(by * g.n_buckets_x + bx)
+            elif len(ys) < n_each and any(wraps(x0 + i, y0 + B - 1, 1) for i in range(B - 1)):
+                ys.append(by * g.n_buckets_x + bx)
+            if corner and len(xs) == n_each and len(ys) == n_each:
+                return xs + ys + corner
+    raise AssertionError("no edge-wrap buckets found: xs %s ys %s corner %s" % (xs, ys, corner))
+
+
+@pytest.mark.parametrize("splat_mode", [4, 3], ids=["skew", "col4"])
+def test_splat_bucket_edge_wraps(gpu, glass_scene, glass_oracle, splat_mode):
+    """Edge-wrapped samples (x, y and the corner source with both) at their raster position in
+    the tile pixels' sums: the skewed-time splat's flagged extra passes and the gather kernels'
+    extra column / row, against the oracle's scatter, bit for bit."""
+    import torch
+    p = _params(glass_scene, 32000, 32000, 16, bounces=1)
+    ids = np.array(_edge_wrap_buckets(p), np.uint32)
+    g = nart_amd.session_geometry(p)
+    tiles = torch.zeros((len(ids), g.tile_size * g.tile_size, 5), dtype=torch.float32, device="cuda")
+    r = nart_amd.HipRenderer(glass_scene, splat_mode=splat_mode)
+    r.render_buckets_async(p, ids, tiles.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ref = glass_oracle.render_buckets(p, ids)
+    got = tiles.cpu().numpy()
+    assert _bits_equal(got, ref), _report(got, ref)
 
 
 @pytest.fixture(scope="module")
