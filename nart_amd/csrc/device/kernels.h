@@ -308,6 +308,7 @@ struct LatinScratch {
     uint32_t n2;  // (spp + 1) / 2 word rows
 };
 #define LATIN_EMIT_SLOTS 16
+#define LATIN_ST_PAD (256 * 8 * 4)  // words read past the last block's states by k_latin_emit
 
 ND size_t latin_row(uint32_t g, uint32_t rows, uint32_t r, uint32_t lane) {
     return ((size_t)g * rows + r) * 64u + lane;
@@ -343,6 +344,9 @@ __global__ __launch_bounds__(256) void k_latin_draws(RenderArgs A, LatinScratch 
 #ifndef NART_LATIN_PF
 #define NART_LATIN_PF 16  // choice words (2 swaps each) loaded one batch ahead of their swaps
 #endif
+#ifndef NART_LATIN_PIPE
+#define NART_LATIN_PIPE 0  // 1: swap i+1's reads issued before swap i's writes (register fix-ups)
+#endif
 __global__ __launch_bounds__(64) void k_latin_perm(RenderArgs A, LatinScratch L) {
     extern __shared__ __attribute__((aligned(16))) uint16_t s_idx[];
     const uint32_t lane = threadIdx.x, g = blockIdx.x;
@@ -357,27 +361,77 @@ __global__ __launch_bounds__(64) void k_latin_perm(RenderArgs A, LatinScratch L)
         constexpr uint32_t PF = NART_LATIN_PF;
         uint32_t cur[PF], nxt[PF];
 #pragma unroll
-        for (uint32_t u = 0; u < PF; ++u) cur[u] = u < n2 ? c[(size_t)u * 64] : 0u;
+        for (uint32_t u = 0; u < PF; ++u) cur[u] = c[(size_t)u * 64];
         for (uint32_t i = 0; i < 2 * n2; ++i) ix[i * 64] = (uint16_t)i;
+#if NART_LATIN_PIPE
+        // Reads one swap ahead: swap i+1's two reads are issued before swap i's writes, so each
+        // wait on LDS overlaps the next swap's issue.  LDS executes a wave's operations in order,
+        // so those reads see every write up to swap i-1; swap i's writes (A[i] <- b, A[c_i] <- a)
+        // are applied to them in registers (positions compared, the later write winning).
+        uint32_t pc = cur[0] & 0xFFFFu;             // c_i of the pending reads
+        uint32_t pa = ix[0], pb = ix[pc * 64];      // raw reads of swap i (issued)
+        uint32_t a1 = 0, b1 = 0, c1 = 0xFFFFFFFFu;  // swap i-1: A[c1] <- a1, A[i-1] <- b1
         for (uint32_t i2 = 0; i2 < n2; i2 += PF) {
 #pragma unroll
             for (uint32_t u = 0; u < PF; ++u) nxt[u] = i2 + PF + u < n2 ? c[(size_t)(i2 + PF + u) * 64] : 0u;
 #pragma unroll
-            for (uint32_t u = 0; u < PF; ++u) {
-#pragma unroll
-                for (uint32_t h = 0; h < 2; ++h) {
-                    const uint32_t i = 2 * (i2 + u) + h;
-                    if (i < n) {
-                        const uint32_t ci = (cur[u] >> (16 * h)) & 0xFFFFu;
-                        const uint16_t t = ix[i * 64];
-                        ix[i * 64] = ix[ci * 64];
-                        ix[ci * 64] = t;
-                    }
+            for (uint32_t q = 0; q < 2 * PF; ++q) {
+                const uint32_t i = 2 * i2 + q;
+                if (i < n) {
+                    const uint32_t cn = q + 1 < 2 * PF ? (cur[(q + 1) / 2] >> (16 * ((q + 1) & 1))) & 0xFFFFu
+                                                       : nxt[0] & 0xFFFFu;
+                    const uint32_t in = i + 1 < n ? i + 1 : i;
+                    const uint32_t na = ix[in * 64], nb = ix[(i + 1 < n ? cn : pc) * 64];  // swap i+1's reads
+                    const uint32_t av = c1 == i ? a1 : pa;
+                    const uint32_t bv = pc == c1 ? a1 : (pc + 1u == i ? b1 : pb);
+                    ix[i * 64] = (uint16_t)bv;  // std::swap(A[i], A[c_i]) (sampling.cpp:81-84)
+                    ix[pc * 64] = (uint16_t)av;
+                    a1 = av;
+                    b1 = bv;
+                    c1 = pc;
+                    pa = na;
+                    pb = nb;
+                    pc = cn;
                 }
             }
 #pragma unroll
             for (uint32_t u = 0; u < PF; ++u) cur[u] = nxt[u];
         }
+#else
+        // Full batches (all 2*PF swaps valid) load the next batch unconditionally (the choice
+        // arrays carry PF padding rows), so that no branch sits between a load and its use: with
+        // guarded loads the compiler waited for every outstanding load (vmcnt(0)) before each
+        // swap, i.e. the prefetch did not hide the HBM latency.
+        uint32_t i2 = 0;
+        for (; 2 * (i2 + PF) <= n; i2 += PF) {
+#pragma unroll
+            for (uint32_t u = 0; u < PF; ++u) nxt[u] = c[(size_t)(i2 + PF + u) * 64];
+#pragma unroll
+            for (uint32_t u = 0; u < PF; ++u) {
+#pragma unroll
+                for (uint32_t h = 0; h < 2; ++h) {
+                    const uint32_t i = 2 * (i2 + u) + h;
+                    const uint32_t ci = (cur[u] >> (16 * h)) & 0xFFFFu;
+                    const uint16_t t = ix[i * 64];
+                    ix[i * 64] = ix[ci * 64];
+                    ix[ci * 64] = t;
+                }
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < PF; ++u) cur[u] = nxt[u];
+        }
+        for (uint32_t u = 0; u < PF; ++u) {  // the partial last batch (cur holds its words)
+            for (uint32_t h = 0; h < 2; ++h) {
+                const uint32_t i = 2 * (i2 + u) + h;
+                if (i < n) {
+                    const uint32_t ci = (cur[u] >> (16 * h)) & 0xFFFFu;
+                    const uint16_t t = ix[i * 64];
+                    ix[i * 64] = ix[ci * 64];
+                    ix[ci * 64] = t;
+                }
+            }
+        }
+#endif
         for (uint32_t j2 = 0; j2 < n2; ++j2)
             so[(size_t)j2 * 64] = (uint32_t)ix[2 * j2 * 64] | ((uint32_t)ix[(2 * j2 + 1) * 64] << 16);
     }
@@ -409,11 +463,24 @@ __global__ __launch_bounds__(256) void k_latin_emit(RenderArgs A, LatinScratch L
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) {
         const uint32_t j2 = j0 + u * RS;
-        cx[u] = live && j2 < n2 ? sx[(size_t)j2 * 64] : 0u;
-        cy[u] = live && j2 < n2 ? sy[(size_t)j2 * 64] : 0u;
+        cx[u] = sx[(size_t)j2 * 64];  // unconditional (padded arrays): see k_latin_perm
+        cy[u] = sy[(size_t)j2 * 64];
     }
-    const uint32_t* stg = L.st + (size_t)blockIdx.x * n * P;
-    for (uint32_t i = t; i < n * P; i += blockDim.x) s_st[i] = stg[i];
+    // stage the block's n*P states: 8 unconditional 16-B loads in flight per thread (the st
+    // region carries LATIN_ST_PAD words of padding), guarded LDS stores
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(L.st + (size_t)blockIdx.x * n * P);
+        uint4* dst = reinterpret_cast<uint4*>(s_st);
+        const uint32_t cnt = n * P / 4;
+        for (uint32_t b0 = 0; b0 < cnt; b0 += 256u * 8u) {
+            uint4 v[8];
+#pragma unroll
+            for (uint32_t u = 0; u < 8; ++u) v[u] = src[b0 + u * 256u + t];
+#pragma unroll
+            for (uint32_t u = 0; u < 8; ++u)
+                if (b0 + u * 256u + t < cnt) dst[b0 + u * 256u + t] = v[u];
+        }
+    }
     __syncthreads();
     if (!live) return;
     const float inv = 1.f / (float)n;
@@ -423,8 +490,8 @@ __global__ __launch_bounds__(256) void k_latin_emit(RenderArgs A, LatinScratch L
 #pragma unroll
         for (uint32_t u = 0; u < U; ++u) {
             const uint32_t j2 = jb + (U + u) * RS;
-            nx[u] = j2 < n2 ? sx[(size_t)j2 * 64] : 0u;
-            ny[u] = j2 < n2 ? sy[(size_t)j2 * 64] : 0u;
+            nx[u] = sx[(size_t)j2 * 64];
+            ny[u] = sy[(size_t)j2 * 64];
         }
 #pragma unroll
         for (uint32_t u = 0; u < U; ++u) {
@@ -1996,6 +2063,9 @@ __global__ __launch_bounds__(256) void k_splat_col4(SplatArgs A) {
 // gather kernels' extra column; the y wrap: the already written rows 0..2R+1, read back and
 // updated at source row B-1).  Per pair the arithmetic is splat_hits_fast + the LUT weight, as
 // in k_splat_col4: bit-identical.
+#ifndef NART_SKEW_PF
+#define NART_SKEW_PF 4  // samples per group; the next group is in flight
+#endif
 template <int R>
 __global__ __launch_bounds__(256) void k_splat_skew(SplatArgs A) {
     constexpr int W = 2 * R + 1, NWR = 2 * R + 2;
@@ -2077,7 +2147,10 @@ __global__ __launch_bounds__(256) void k_splat_skew(SplatArgs A) {
     float fy = 0.f, ybA = 0.f, ybB = 0.f;  // per source row: fy, and the window's first image row
                                            // without / with the y wrap (splat_hits_fast)
     float fx = 0.f;
-    // one sample into the window rows wb .. wb+2R
+    // one sample into the window rows wb .. wb+2R (splat_hits_fast + the LUT weight).  The
+    // rows' image coordinates ys_k = yb + k (exact small integers) and the distance terms are
+    // formed two rows per packed instruction: (ys_k + 0.5) - scy and d2 = dx2 + distY^2 are
+    // the same IEEE operations per row; ys_k + 1 is ys_{k+1}.
     auto splat_w = [&](float2 uv, float4 L) {
         const float scx = fx + uv.x, scy = fy + uv.y;
         const float xs = scx >= edgeX ? xsB : xsA;
@@ -2086,17 +2159,25 @@ __global__ __launch_bounds__(256) void k_splat_skew(SplatArgs A) {
         const float dx2 = distX * distX;
         const float yb = scy >= edgeY ? ybB : ybA;
         const float loy = scy - fw, hiy = scy + fw;
+        constexpr int WP = (W + 2) / 2;  // row pairs covering ys_0 .. ys_W
+        float ys[2 * WP], d2[2 * WP];
+#pragma unroll
+        for (int k = 0; k < WP; ++k) {
+            const nd_f2v y2 = nd_f2v{yb, yb} + nd_f2v{(float)(2 * k), (float)(2 * k + 1)};
+            const nd_f2v dy = (y2 + nd_f2v{0.5f, 0.5f}) - nd_f2v{scy, scy};
+            const nd_f2v dd = nd_f2v{dx2, dx2} + dy * dy;
+            ys[2 * k] = y2.x;
+            ys[2 * k + 1] = y2.y;
+            d2[2 * k] = dd.x;
+            d2[2 * k + 1] = dd.y;
+        }
 #pragma unroll
         for (int k = 0; k < W; ++k) {
-            const float ys = yb + (float)k;
-            const bool hit = xhit && loy < ys + 1.f && ys < hiy;
-            const float distY = (ys + 0.5f) - scy;
-            const float d2 = dx2 + distY * distY;
-            int cell = (int)(__float_as_uint(d2) >> 16) - lut_b0;
-            cell = cell < 0 ? 0 : (cell > lut_last ? lut_last : cell);
-            const float4 e = s_lut[cell];
-            const float w = d2 >= e.x ? e.z : e.y;
+            const bool hit = xhit && loy < ys[k + 1] && ys[k] < hiy;
             if (hit) {
+                const int cell = max(0, min((int)(__float_as_uint(d2[k]) >> 16) - lut_b0, lut_last));
+                const float4 e = s_lut[cell];
+                const float w = d2[k] >= e.x ? e.z : e.y;
                 const nd_f2v w2 = nd_f2v{w, w};
                 cxy[k] += nd_f2v{L.x, L.y} * w2;
                 czw[k] += nd_f2v{L.z, L.w} * w2;
@@ -2109,7 +2190,7 @@ __global__ __launch_bounds__(256) void k_splat_skew(SplatArgs A) {
         const float2* sp = A.samples + first;
         const float4* lp = A.Lout + first;
         fx = (float)(x0 + (uint32_t)sx + A.fb);
-        constexpr uint32_t PF = 4;
+        constexpr uint32_t PF = NART_SKEW_PF;
         uint32_t i = 0;
         float2 nu[PF];
         float4 nL[PF];

@@ -878,8 +878,11 @@ int launch_latin(nart_ctx* ctx, const RenderArgs& ra, hipStream_t st) {
     const uint32_t groups = (ra.n_slots + 63) / 64;
     LatinScratch ls;
     ls.n2 = (ra.spp + 1) / 2;
-    const size_t words = (size_t)groups * 64 * ls.n2;
-    const size_t stw = (size_t)((ra.n_slots + LATIN_EMIT_SLOTS - 1) / LATIN_EMIT_SLOTS) * LATIN_EMIT_SLOTS * ra.spp;
+    // + padding rows per array: k_latin_perm / k_latin_emit load a batch of words ahead,
+    // unconditionally
+    const size_t words = (size_t)groups * 64 * ls.n2 + (size_t)std::max(NART_LATIN_PF, 2 * LATIN_EMIT_U * 16) * 64;
+    const size_t stw = (size_t)((ra.n_slots + LATIN_EMIT_SLOTS - 1) / LATIN_EMIT_SLOTS) * LATIN_EMIT_SLOTS * ra.spp +
+                       LATIN_ST_PAD;
     const bool three = ra.spp >= 2 && ra.spp <= 1024 && (4 * words + stw) * 4 <= ctx->cap_samples * sizeof(float4) &&
                        (latin_env == 3 || (latin_env < 0 && ra.spp > 256));
     if (three) {
