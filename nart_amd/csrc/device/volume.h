@@ -19,10 +19,11 @@ ND f3 uniform_sample_sphere(f2 smp) {  // sampling.cpp:33-45 (pdf unused by the 
     return F3(sinTheta * cosPhi, sinTheta * sinPhi, cosTheta);
 }
 
-NHD float dg_at(const DMedium& m, uint32_t x, uint32_t y, uint32_t z) {  // media.cpp:3-7
-    return m.density[(m.rx * m.ry * z) + (m.rx * y) + x];
+NHD float dg_at(const DMedium& m, const float* dens, uint32_t x, uint32_t y, uint32_t z) {  // media.cpp:3-7
+    return dens[(m.rx * m.ry * z) + (m.rx * y) + x];
 }
-NHD float dg_lookup(const DMedium& m, f3 p) {  // media.cpp:10-45
+// dens: the grid (m.density, or its LDS copy)
+NHD float dg_lookup(const DMedium& m, const float* dens, f3 p) {  // media.cpp:10-45
     const float x = gmin(gmax(0.f, p.x), 0.999f) * (float)((int)m.rx - 1);
     const uint32_t loX = (uint8_t)(uint32_t)x, hiX = (uint8_t)(loX + 1);
     const float xD = (x - (float)loX);
@@ -32,10 +33,10 @@ NHD float dg_lookup(const DMedium& m, f3 p) {  // media.cpp:10-45
     const float z = gmin(gmax(0.f, p.z), 0.999f) * (float)((int)m.rz - 1);
     const uint32_t loZ = (uint8_t)(uint32_t)z, hiZ = (uint8_t)(loZ + 1);
     const float zD = (z - (float)loZ);
-    const float x0 = gmix(dg_at(m, loX, loY, loZ), dg_at(m, hiX, loY, loZ), xD);
-    const float x1 = gmix(dg_at(m, loX, loY, hiZ), dg_at(m, hiX, loY, hiZ), xD);
-    const float x2 = gmix(dg_at(m, loX, hiY, loZ), dg_at(m, hiX, hiY, loZ), xD);
-    const float x3 = gmix(dg_at(m, loX, hiY, hiZ), dg_at(m, hiX, hiY, hiZ), xD);
+    const float x0 = gmix(dg_at(m, dens, loX, loY, loZ), dg_at(m, dens, hiX, loY, loZ), xD);
+    const float x1 = gmix(dg_at(m, dens, loX, loY, hiZ), dg_at(m, dens, hiX, loY, hiZ), xD);
+    const float x2 = gmix(dg_at(m, dens, loX, hiY, loZ), dg_at(m, dens, hiX, hiY, loZ), xD);
+    const float x3 = gmix(dg_at(m, dens, loX, hiY, hiZ), dg_at(m, dens, hiX, hiY, hiZ), xD);
     const float y0 = gmix(x0, x2, yD);
     const float y1 = gmix(x1, x3, yD);
     return gmix(y0, y1, zD);
@@ -45,7 +46,7 @@ struct MajIter {  // RayMajorantIterator (media.cpp:138-255) for a width-1 grid
     float tCurrent, tMax;
     uint32_t idx;
     f3 next, cross;
-    int step[3];
+    uint32_t stepPos;  // bit i: step[i] > 0 (only the sign of the step is ever used)
 };
 
 // Medium::SampleRay (media.cpp:281-324) + the iterator constructor.
@@ -96,9 +97,7 @@ ND bool medium_sample_ray(const DMedium& m, f3 o, f3 d, MajIter& it) {
         if (g == 0.f) t3[i] = __builtin_inff();
     }
     it.next = muls(mul(F3(t3[0], t3[1], t3[2]), bs), 1.f);
-    it.step[0] = gD.x < 0.f ? -1 : 1;
-    it.step[1] = gD.y < 0.f ? -1 : 1;
-    it.step[2] = gD.z < 0.f ? -1 : 1;
+    it.stepPos = (gD.x < 0.f ? 0u : 1u) | (gD.y < 0.f ? 0u : 2u) | (gD.z < 0.f ? 0u : 4u);
     return true;
 }
 
@@ -112,19 +111,18 @@ ND bool maj_next(const DMedium& m, MajIter& it, float& sigma, float& t0, float& 
     const int index = (choice == 0 || choice == 4) ? 2 : (choice == 1 || choice == 3) ? 1 : 0;
     const float dt = index == 0 ? it.next.x : index == 1 ? it.next.y : it.next.z;
     if (it.idx > 7) return false;  // past the Medium object: undefined in the reference
+    // selects only (an indexed form made the compiler keep the iterator in scratch memory)
     float sm = m.maj[0];
 #pragma unroll
-    for (int j = 1; j < 8; ++j)
-        if ((int)it.idx == j) sm = m.maj[j];
+    for (int j = 1; j < 8; ++j) sm = (int)it.idx == j ? m.maj[j] : sm;
     sigma = sm;
     t0 = it.tCurrent;
     t1 = it.tCurrent + dt;
-    it.next = sub(it.next, F3(dt, dt, dt));
-    if (index == 0) it.next.x = it.cross.x;
-    else if (index == 1) it.next.y = it.cross.y;
-    else it.next.z = it.cross.z;
-    const int st = index == 0 ? it.step[0] : index == 1 ? it.step[1] : it.step[2];
-    it.idx += st > 0 ? 1u : 0u;
+    const float nx = it.next.x - dt, ny = it.next.y - dt, nz = it.next.z - dt;
+    it.next.x = index == 0 ? it.cross.x : nx;
+    it.next.y = index == 1 ? it.cross.y : ny;
+    it.next.z = index == 2 ? it.cross.z : nz;
+    it.idx += (it.stepPos >> index) & 1u;
     it.tCurrent += dt;
     return true;
 }
@@ -161,7 +159,7 @@ ND f4 li_volume(const DScene& S, const RenderArgs& A, uint32_t& rng, f3 o, f3 d,
                     const f3 bmin = F3(m.bmin[0], m.bmin[1], m.bmin[2]);
                     const f3 bs = sub(F3(m.bmax[0], m.bmax[1], m.bmax[2]), bmin);
                     const f3 q0 = sub(p, bmin);
-                    const float density = dg_lookup(m, F3(q0.x / bs.x, q0.y / bs.y, q0.z / bs.z));
+                    const float density = dg_lookup(m, m.density, F3(q0.x / bs.x, q0.y / bs.y, q0.z / bs.z));
                     const float sa = m.sigma_a * density, ss = m.sigma_s * density;
                     const float pAbsorb = sa / sigma;
                     const float pScatter = ss / sigma;
@@ -255,10 +253,12 @@ __global__ __launch_bounds__(256) void k_render_volume_sm(DScene S, RenderArgs A
         logf_table((int)threadIdx.x, invc, logc);
         s_logf[threadIdx.x] = make_double2(invc, logc);
     }
-    DMedium mloc = S.medium;
+    // the medium stays in the kernel arguments (a local copy with its density pointer swapped
+    // lived in scratch memory: every field read in the loop was a scratch load)
+    const float* dens = S.medium.density;
     if (A.lds_nodes) {
         for (uint32_t i = threadIdx.x; i < A.lds_nodes; i += blockDim.x) s_dens[i] = S.medium.density[i];
-        mloc.density = s_dens;
+        dens = s_dens;
     }
     __syncthreads();
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -270,7 +270,7 @@ __global__ __launch_bounds__(256) void k_render_volume_sm(DScene S, RenderArgs A
     const SlotSO so = A.slot_so[slot];
     const float2* smp = A.samples + so.first;
     float4* out = A.Lout + so.first;
-    const DMedium& m = mloc;
+    const DMedium& m = S.medium;
     const f3 beta = F3(1.f, 1.f, 1.f);
     enum { P_SAMPLE, P_RAY, P_MAJ, P_COLL, P_ESC };
     uint32_t work = 0, s = 0, bounce = 0;
@@ -328,7 +328,7 @@ __global__ __launch_bounds__(256) void k_render_volume_sm(DScene S, RenderArgs A
                     const f3 bmin = F3(m.bmin[0], m.bmin[1], m.bmin[2]);
                     const f3 bs = sub(F3(m.bmax[0], m.bmax[1], m.bmax[2]), bmin);
                     const f3 q0 = sub(p, bmin);
-                    const float density = dg_lookup(m, F3(q0.x / bs.x, q0.y / bs.y, q0.z / bs.z));
+                    const float density = dg_lookup(m, dens, F3(q0.x / bs.x, q0.y / bs.y, q0.z / bs.z));
                     const float sa = m.sigma_a * density, ss = m.sigma_s * density;
                     const float pAbsorb = sa / sigma;
                     const float pScatter = ss / sigma;

@@ -30,7 +30,7 @@ struct nart_ctx {
     uint32_t num_nodes = 0;
     int variant = 0;
     // 3 four pixels per lane (default), 2/1/0 one pixel per lane
-    int splat_mode = 4;
+    int splat_mode = -1;  // -1: automatic (render_buckets)
     bool counters = false;
     bool has_env = false;  // scene has an environment light (selects the k_render build)
     // scene buffers
@@ -253,9 +253,9 @@ int build_medium(nart_ctx* ctx, const nart_medium& bm, DMedium& m) {
     float majorant = 0.f;
     for (uint32_t k = 0; k < z1; ++k)
         for (uint32_t j = 0; j < y1; ++j)
-            for (uint32_t i = 0; i < x1; ++i) majorant = gmax(majorant, dg_at(m, i, j, k));
+            for (uint32_t i = 0; i < x1; ++i) majorant = gmax(majorant, dg_at(m, m.density, i, j, k));
     for (int c = 0; c < 8; ++c)
-        majorant = gmax(majorant, dg_lookup(m, F3((c & 4) ? 1.f : 0.f, (c & 2) ? 1.f : 0.f, (c & 1) ? 1.f : 0.f)));
+        majorant = gmax(majorant, dg_lookup(m, m.density, F3((c & 4) ? 1.f : 0.f, (c & 2) ? 1.f : 0.f, (c & 1) ? 1.f : 0.f)));
     m.maj[0] = majorant * sigma_maj;
     m.maj[1] = sigma_maj;
     for (int i = 0; i < 3; ++i) {
@@ -936,8 +936,18 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
     const bool lut_ok = lut_env && thr_ok && splat_lut(table + 64, table, lut, lut_b0);
     // skewed-time splat (k_splat_skew, pixel-major samples) where its preconditions hold, else
     // k_splat_col4 / k_splat over the sample-major layout
+    // It runs one lane per tile column for ~W*B steps, so its time is one wave's latency once the
+    // launch has fewer than ~2 waves per SIMD: small shards keep k_splat_col4 (C5 1/8 shard:
+    // 54 ms skewed vs 23 ms col4; whole frame 72 vs 113 ms).  NART_SKEW_MIN_WAVES: waves per SIMD.
     const uint32_t B = p->bucket_size, tile = B + 2 * g.filter_bounds;
-    const bool skew = ctx->splat_mode >= 4 && lut_ok && (B & (B - 1)) == 0 && B <= 32 && tile <= 64 &&
+    static const double skew_min =
+        std::getenv("NART_SKEW_MIN_WAVES") ? std::atof(std::getenv("NART_SKEW_MIN_WAVES")) : 2.0;
+    int n_cus = 0;
+    HIPCHK(hipDeviceGetAttribute(&n_cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    const double skew_waves = tile <= 64 ? (double)((n + 64 / tile - 1) / (64 / tile)) : 0.0;
+    // splat mode -1 (default): 4 where the launch is large enough, else 3; an explicit 4 forces it
+    const int splat_mode = ctx->splat_mode >= 0 ? ctx->splat_mode : (skew_waves >= skew_min * 4.0 * n_cus ? 4 : 3);
+    const bool skew = splat_mode >= 4 && lut_ok && (B & (B - 1)) == 0 && B <= 32 && tile <= 64 &&
                       g.filter_bounds >= 1 && g.filter_bounds <= 3;
     if (lut_ok) {
         if (!ctx->d_lut) HIPCHK(hipMalloc(&ctx->d_lut, SPLAT_LUT_MAX * sizeof(float4)));
@@ -1043,7 +1053,6 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
             sa.invFw = (m == 0.5f) ? 1.f / p->filter_width : 0.f;
         }
         uint64_t nthreads = (uint64_t)nbk * tpx;
-        const int splat_mode = ctx->splat_mode;
         const dim3 sg((uint32_t)((nthreads + 255) / 256));
 #ifndef NART_SPLAT_NP
 #define NART_SPLAT_NP 4
@@ -1309,7 +1318,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
         const int var = std::atoi(v);
         if (var == 0 || var == 2 || var == 3) ctx->variant = var;
     }
-    if (const char* v = std::getenv("NART_SPLAT_MODE")) ctx->splat_mode = std::max(0, std::min(4, std::atoi(v)));
+    if (const char* v = std::getenv("NART_SPLAT_MODE")) ctx->splat_mode = std::max(-1, std::min(4, std::atoi(v)));
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device_id || device_id < 0) {
         delete ctx;
@@ -1547,8 +1556,8 @@ int nart_hip_set_splat_mode(nart_ctx* ctx, int mode) {
     if (!ctx) return NART_E_INVALID;
     for (nart_ctx* c : ctx->subs)
         if (int rc = nart_hip_set_splat_mode(c, mode)) return fail(ctx, rc, c->err);
-    if (mode < 0 || mode > 4)
-        return fail(ctx, NART_E_UNSUPPORTED, "splat mode must be 0-4 (4 skewed-time tile columns, 3 four pixels per "
+    if (mode < -1 || mode > 4)
+        return fail(ctx, NART_E_UNSUPPORTED, "splat mode must be -1 (automatic) or 0-4 (4 skewed-time tile columns, 3 four pixels per "
                                              "lane, 2-0 one pixel per lane; the LDS-staged and tile-column-sweep modes "
                                              "were retired, DESIGN.md)");
     ctx->splat_mode = mode;

@@ -354,6 +354,19 @@ def test_splat_bucket_and_filter_sizes(gpu, glass_scene, glass_oracle, bucket, f
     assert _bits_equal(g, o), _report(g, o)
 
 
+@pytest.mark.parametrize("which", ["glass", "materials", "env", "volume"])
+def test_skew_splat_frames(gpu, glass_scene, materials_scene, env_scene, volume_scenes, which):
+    """The skewed-time splat (forced: by default it runs only on launches of >= 2 waves per
+    SIMD) over the pixel-major sample layout, on frames of the path and volume integrators with
+    filter widths 2 and 1.5 and ragged edge buckets, against the oracle's framebuffer."""
+    sc = {"glass": glass_scene, "materials": materials_scene, "env": env_scene,
+          "volume": volume_scenes["c5"]}[which]
+    p = _params(sc, 72, 40, 16)
+    g = nart_amd.HipRenderer(sc, splat_mode=4).render(p)
+    r = oracle.Oracle(sc).render(p)
+    assert _bits_equal(g, r), _report(g, r)
+
+
 def _edge_wrap_buckets(p, n_each=2):
     """Full buckets of a wide frame whose last-column / last-row samples round onto the next
     bucket's origin (render.cpp:52-61: splatted through glm::mod into the start of their own
