@@ -241,8 +241,10 @@ __global__ __launch_bounds__(256) void k_render_volume(DScene S, RenderArgs A) {
 // segment), and a lane whose sample ends starts its next sample at once, so the wave costs about
 // max_lane sum_s(collisions).  Each lane performs exactly the RNG draws and float operations of
 // li_volume in the same order: the output is bit-identical.
-template <bool COUNT>
-__global__ __launch_bounds__(256) void k_render_volume_sm(DScene S, RenderArgs A) {
+// WV: minimum waves per SIMD requested from the register allocator (dispatch_volume: 4 on
+// throughput-bound launches, 1 on small shards)
+template <bool COUNT, int WV>
+__global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderArgs A) {
     // A.lds_nodes != 0: the density grid (that many floats) is staged in LDS
     extern __shared__ float s_dens[];
     // glibc logf's (invc, logc) table: one LDS read per tentative collision instead of a

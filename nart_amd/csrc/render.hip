@@ -755,11 +755,17 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     const uint32_t nd = ctx->scene.medium.present ? ctx->scene.medium.rx * ctx->scene.medium.ry * ctx->scene.medium.rz : 0;
     b.lds_nodes = (sm && vol_lds && nd <= 4096u) ? nd : 0u;
     const size_t dl = (size_t)b.lds_nodes * sizeof(float);
+    // occupancy: launches of >= 8 rounds of resident waves use the 4-waves-per-SIMD build (C5 frame,
+    // 10.5 rounds: 134 -> 122 ms); smaller ones keep the unconstrained build, whose lanes' serial
+    // chains are shorter (C5 1/2, 1/4, 1/8 shards: 79 / 74 / 71 ms vs 83 / 80 / 76 with 4 waves;
+    // profiles/r03h_vol_w4_ab.log)
+    int cus = 0, per_cu = 0;
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_render_volume_sm<false, 1>, 256, dl));
+    const uint32_t resident = (uint32_t)std::max(1, cus * std::max(per_cu, 1));
+    static const double w4_rounds = std::getenv("NART_VOL_W4_ROUNDS") ? std::atof(std::getenv("NART_VOL_W4_ROUNDS")) : 8.0;
+    const bool w4 = (double)blocks / (double)resident >= w4_rounds;
     if (queue_mode() == 2) {
-        int cus = 0, per_cu = 0;
-        HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_render_volume_sm<false>, 256, 0));
-        const uint32_t resident = (uint32_t)std::max(1, cus * std::max(per_cu, 1));
         const uint32_t n = a.n_slots;
         if (blocks > resident && (double)n / (256.0 * resident) < 12.0 && a.spp > 4) {
             int rc = ensure_queue(ctx, n);
@@ -767,7 +773,7 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             RenderArgs pb = b;
             pb.spp = 4;
             pb.cost = ctx->d_cost;
-            if (sm) hipLaunchKernelGGL((k_render_volume_sm<false>), dim3(blocks), block, dl, st, ctx->scene, pb);
+            if (sm) hipLaunchKernelGGL((k_render_volume_sm<false, 1>), dim3(blocks), block, dl, st, ctx->scene, pb);
             else hipLaunchKernelGGL((k_render_volume<false>), dim3(blocks), block, 0, st, ctx->scene, pb);
             rc = sort_groups_by_cost(ctx, n, ctx->d_queue, st);
             if (rc) return rc;
@@ -775,8 +781,9 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
         }
     }
     if (sm) {
-        if (ctx->counters) hipLaunchKernelGGL((k_render_volume_sm<true>), dim3(blocks), block, dl, st, ctx->scene, b);
-        else hipLaunchKernelGGL((k_render_volume_sm<false>), dim3(blocks), block, dl, st, ctx->scene, b);
+        if (ctx->counters) hipLaunchKernelGGL((k_render_volume_sm<true, 1>), dim3(blocks), block, dl, st, ctx->scene, b);
+        else if (w4) hipLaunchKernelGGL((k_render_volume_sm<false, 4>), dim3(blocks), block, dl, st, ctx->scene, b);
+        else hipLaunchKernelGGL((k_render_volume_sm<false, 1>), dim3(blocks), block, dl, st, ctx->scene, b);
     } else {
         if (ctx->counters) hipLaunchKernelGGL((k_render_volume<true>), dim3(blocks), block, 0, st, ctx->scene, b);
         else hipLaunchKernelGGL((k_render_volume<false>), dim3(blocks), block, 0, st, ctx->scene, b);
