@@ -140,8 +140,8 @@ int nart_hip_context_bvh(const nart_ctx* ctx, nart_bvh_info* out, double* build_
    1 (the wavefront variant, 2x slower) was retired: NART_E_UNSUPPORTED. */
 int nart_hip_set_variant(nart_ctx* ctx, int variant);
 
-/* Splat kernel (all bit-identical): -1 = automatic (the default: 4 when the launch fills >= 2
-   waves per SIMD, else 3), 4 = skewed-time tile columns over the pixel-major sample layout (each
+/* Splat kernel (all bit-identical): -1 = automatic (the default: 4 when the launch fills >= 1
+   wave per SIMD, else 3), 4 = skewed-time tile columns over the pixel-major sample layout (each
    sample fetched once per bucket), 3 = four tile pixels per lane over the sample-major layout;
    2, 1, 0 = one tile pixel per lane with the compare-only / threshold / direct filter-index
    arithmetic.  Modes fall back to a lower one where their preconditions (power-of-two buckets

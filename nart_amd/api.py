@@ -338,7 +338,7 @@ class HipRenderer:
         self._check(self._lib.nart_hip_set_variant(self._ctx, int(variant)))
 
     def set_splat_mode(self, mode):
-        """-1 = automatic (default: the skewed-time splat on launches of >= 2 waves per SIMD, else
+        """-1 = automatic (default: the skewed-time splat on launches of >= 1 wave per SIMD, else
         four tile pixels per lane), 4 = skewed-time splat, 3 = four tile pixels per lane, 2-0 = one
         pixel per lane (include/nart_hip.h); identical results."""
         self._check(self._lib.nart_hip_set_splat_mode(self._ctx, int(mode)))

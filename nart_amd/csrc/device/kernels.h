@@ -2066,7 +2066,11 @@ __global__ __launch_bounds__(256) void k_splat_col4(SplatArgs A) {
 #ifndef NART_SKEW_PF
 #define NART_SKEW_PF 4  // samples per group; the next group is in flight
 #endif
-template <int R>
+// NB bands: a bucket's tile rows split into NB bands of ceil(T/NB) rows, each band a unit of T
+// lanes with its own source rows [band start - 2R, band end - 1] (the 2R rows before a band are
+// read by both neighbours): NB times the waves for ~1/NB of the steps each, for launches whose
+// time is otherwise the waves' latency (VALU ~30 % busy at 2.7 waves per SIMD).
+template <int R, int NB>
 __global__ __launch_bounds__(256) void k_splat_skew(SplatArgs A) {
     constexpr int W = 2 * R + 1, NWR = 2 * R + 2;
     extern __shared__ __attribute__((aligned(16))) float4 s_dyn4[];
@@ -2077,8 +2081,9 @@ __global__ __launch_bounds__(256) void k_splat_skew(SplatArgs A) {
     if (threadIdx.x < 8u * PB) s_flag[threadIdx.x] = 0u;
     __syncthreads();
     const uint32_t lb = l / T, tx = l % T;
-    const uint32_t bi = (blockIdx.x * 4u + wv) * PB + lb;
+    const uint32_t unit = (blockIdx.x * 4u + wv) * PB + lb, bi = unit / NB, band = unit % NB;
     const bool live = lb < PB && bi < A.n_buckets;
+    const int rpb = ((int)T + NB - 1) / NB, tr0 = (int)band * rpb, tr1 = min((int)T, tr0 + rpb);  // tile rows
     uint32_t* flag = s_flag + 2u * (wv * PB + (lb < PB ? lb : 0u));
     uint32_t bid = 0, x0 = 0, y0 = 0, base = 0;
     int bw = 0, bh = 0;
@@ -2123,16 +2128,19 @@ __global__ __launch_bounds__(256) void k_splat_skew(SplatArgs A) {
         czw[k] = nd_f2v{0.f, 0.f};
         cws[k] = 0.f;
     }
-    int wb = 0;  // tile row of cxy[0]
+    const int sr0 = max(0, tr0 - 2 * R);  // first source row of the band
+    int wb = sr0;                          // tile row of cxy[0]
     const uint32_t tpx = T * T;
     float* out = A.tiles + ((uint64_t)bi * tpx + tx) * 5;  // + ty * T * 5
-    auto retire = [&]() {
-        float* o = out + (size_t)wb * T * 5;
-        o[0] = cxy[0].x;
-        o[1] = cxy[0].y;
-        o[2] = czw[0].x;
-        o[3] = czw[0].y;
-        o[4] = cws[0];
+    auto retire = [&]() {  // rows outside the band belong to a neighbour unit
+        if (wb >= tr0 && wb < tr1) {
+            float* o = out + (size_t)wb * T * 5;
+            o[0] = cxy[0].x;
+            o[1] = cxy[0].y;
+            o[2] = czw[0].x;
+            o[3] = czw[0].y;
+            o[4] = cws[0];
+        }
 #pragma unroll
         for (int k = 0; k + 1 < W; ++k) {
             cxy[k] = cxy[k + 1];
@@ -2272,24 +2280,28 @@ __global__ __launch_bounds__(256) void k_splat_skew(SplatArgs A) {
                 for (int c = 0; c < 5; ++c) out[(size_t)k * T * 5 + c] = acc[k][c];
     };
     const bool xwrap_lane = bw == B && (int)tx <= 2 * R + 1 && bw - 1 > (int)tx;
-    const int tmax = W * (B - 1) + (B - 1);
-    for (int t = 0; t <= tmax; ++t) {
+    const int sr1 = min(bh - 1, tr1 - 1);  // last source row of the band
+    const int tmax = W * (min(B, rpb + 2 * R) - 1) + (B - 1);  // wave-uniform step count
+    for (int t0 = 0; t0 <= tmax; ++t0) {
+        const int t = t0 + W * sr0;
         const int d = (((int)tx - t) % W + W) % W;
         const int sx = (int)tx - d, sy = (t - sx) / W;
-        if (sx < 0 || sx >= bw || sy < 0 || sy >= bh) continue;
+        if (sx < 0 || sx >= bw || sy < sr0 || sy > sr1) continue;
         while (wb < sy) retire();
         fy = (float)(y0 + (uint32_t)sy + A.fb);
         ybA = (float)(y0 + (uint32_t)sy);
         ybB = (float)(y0 + A.B + (uint32_t)sy);
         source_pass(sy, sx);
-        const bool ylast = bh == B && sy == B - 1;
-        if (ylast && ((flagY >> sx) & 1u)) ywrap_pass(sx);
-        if (xwrap_lane && sx == (int)tx && ((flagX >> sy) & 1u)) {  // the gather kernels' extra column
-            source_pass(sy, bw - 1);
-            if (ylast && ((flagY >> (bw - 1)) & 1u)) ywrap_pass(bw - 1);
-        }
+        if (xwrap_lane && sx == (int)tx && ((flagX >> sy) & 1u)) source_pass(sy, bw - 1);  // the gather kernels' extra column
     }
-    while (wb < (int)T) retire();
+    while (wb < tr1) retire();
+    // y wrap: last-row samples into tile rows 0 .. 2R+1 (the first band's), after all their other
+    // sources, in the raster order of their source columns, the extra column last
+    if (tr0 == 0 && bh == B) {
+        for (int sx = max(0, (int)tx - 2 * R); sx <= min(bw - 1, (int)tx); ++sx)
+            if ((flagY >> sx) & 1u) ywrap_pass(sx);
+        if (xwrap_lane && ((flagY >> (bw - 1)) & 1u)) ywrap_pass(bw - 1);
+    }
 }
 
 // ---------------------------------------------------------------- combine

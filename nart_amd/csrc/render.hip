@@ -952,8 +952,20 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
     int n_cus = 0;
     HIPCHK(hipDeviceGetAttribute(&n_cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
     const double skew_waves = tile <= 64 ? (double)((n + 64 / tile - 1) / (64 / tile)) : 0.0;
-    // splat mode -1 (default): 4 where the launch is large enough, else 3; an explicit 4 forces it
-    const int splat_mode = ctx->splat_mode >= 0 ? ctx->splat_mode : (skew_waves >= skew_min * 4.0 * n_cus ? 4 : 3);
+    // splat mode -1 (default): 4 where the launch is large enough, else 3; an explicit 4 forces it.
+    // Launches of 1-2 waves per SIMD split each bucket's tile rows into two bands (twice the waves
+    // for ~2/3 of the steps each): C5 1/2 shard 60 -> 49 ms (k_splat_col4: 62); a whole frame keeps
+    // one band (C5 73 vs 92 ms with two).  Below 1 wave per SIMD k_splat_col4 is faster (C5 1/4,
+    // 1/8 shards: 36 / 23 ms vs 41 / 37 with two bands; profiles/r03k_skew_band_ab.log).
+    // The two-band range is the volume integrator's only: the path kernels lose more to the
+    // pixel-major layout there than the splat gains (C3 1/2 shard: path kernels 196 -> 208 ms,
+    // splat 17 -> 13 ms; profiles/r03k_shard_scaling_c3.log).
+    const double skew_from = p->integrator == NART_INTEGRATOR_VOLUME ? 0.5 * skew_min : skew_min;
+    const int splat_mode = ctx->splat_mode >= 0 ? ctx->splat_mode : (skew_waves >= skew_from * 4.0 * n_cus ? 4 : 3);
+    // NART_SKEW_BANDS (read per call): 1 or 2 forces the band count
+    const char* be = std::getenv("NART_SKEW_BANDS");
+    const uint32_t skew_bands = be && std::atoi(be) > 0 ? (std::atoi(be) >= 2 ? 2u : 1u)
+                                                          : (skew_waves >= skew_min * 4.0 * n_cus ? 1u : 2u);
     const bool skew = splat_mode >= 4 && lut_ok && (B & (B - 1)) == 0 && B <= 32 && tile <= 64 &&
                       g.filter_bounds >= 1 && g.filter_bounds <= 3;
     if (lut_ok) {
@@ -1068,11 +1080,16 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         // splat modes (all bit-identical, mode 3 the default): 3 four tile pixels per lane; 2 / 1 / 0
         // one tile pixel per lane with the compare-only / threshold / direct filter-index arithmetic
         if (skew) {
-            const uint32_t pb = 64u / g.tile_size, nblk = (nbk + 4 * pb - 1) / (4 * pb);
+            const uint32_t nb = skew_bands;  // tile-row bands per bucket (k_splat_skew's NB)
+            const uint32_t pb = 64u / g.tile_size, nblk = (nbk * nb + 4 * pb - 1) / (4 * pb);
             const size_t lds = lut.size() * sizeof(float4) + 8u * pb * sizeof(uint32_t);
-            if (g.filter_bounds == 1) hipLaunchKernelGGL(k_splat_skew<1>, dim3(nblk), dim3(256), lds, st, sa);
-            else if (g.filter_bounds == 2) hipLaunchKernelGGL(k_splat_skew<2>, dim3(nblk), dim3(256), lds, st, sa);
-            else hipLaunchKernelGGL(k_splat_skew<3>, dim3(nblk), dim3(256), lds, st, sa);
+            const int fbk = (int)g.filter_bounds * 2 + (int)nb - 1;
+            if (fbk == 2) hipLaunchKernelGGL((k_splat_skew<1, 1>), dim3(nblk), dim3(256), lds, st, sa);
+            else if (fbk == 3) hipLaunchKernelGGL((k_splat_skew<1, 2>), dim3(nblk), dim3(256), lds, st, sa);
+            else if (fbk == 4) hipLaunchKernelGGL((k_splat_skew<2, 1>), dim3(nblk), dim3(256), lds, st, sa);
+            else if (fbk == 5) hipLaunchKernelGGL((k_splat_skew<2, 2>), dim3(nblk), dim3(256), lds, st, sa);
+            else if (fbk == 6) hipLaunchKernelGGL((k_splat_skew<3, 1>), dim3(nblk), dim3(256), lds, st, sa);
+            else hipLaunchKernelGGL((k_splat_skew<3, 2>), dim3(nblk), dim3(256), lds, st, sa);
         } else if (sa.thr && sa.invB != 0.f && splat_mode >= 3)
         {
             if (sa.lut)

@@ -354,11 +354,14 @@ def test_splat_bucket_and_filter_sizes(gpu, glass_scene, glass_oracle, bucket, f
     assert _bits_equal(g, o), _report(g, o)
 
 
+@pytest.mark.parametrize("bands", [1, 2])
 @pytest.mark.parametrize("which", ["glass", "materials", "env", "volume"])
-def test_skew_splat_frames(gpu, glass_scene, materials_scene, env_scene, volume_scenes, which):
-    """The skewed-time splat (forced: by default it runs only on launches of >= 2 waves per
-    SIMD) over the pixel-major sample layout, on frames of the path and volume integrators with
-    filter widths 2 and 1.5 and ragged edge buckets, against the oracle's framebuffer."""
+def test_skew_splat_frames(gpu, glass_scene, materials_scene, env_scene, volume_scenes, which, bands, monkeypatch):
+    """The skewed-time splat (forced: by default it runs only on launches of >= 1 wave per SIMD)
+    over the pixel-major sample layout, with one and two tile-row bands per bucket, on frames of
+    the path and volume integrators with filter widths 2 and 1.5 and ragged edge buckets, against
+    the oracle's framebuffer."""
+    monkeypatch.setenv("NART_SKEW_BANDS", str(bands))
     sc = {"glass": glass_scene, "materials": materials_scene, "env": env_scene,
           "volume": volume_scenes["c5"]}[which]
     p = _params(sc, 72, 40, 16)
@@ -396,12 +399,14 @@ def _edge_wrap_buckets(p, n_each=2):
     raise AssertionError("no edge-wrap buckets found: xs %s ys %s corner %s" % (xs, ys, corner))
 
 
-@pytest.mark.parametrize("splat_mode", [4, 3], ids=["skew", "col4"])
-def test_splat_bucket_edge_wraps(gpu, glass_scene, glass_oracle, splat_mode):
+@pytest.mark.parametrize("splat_mode,bands", [(4, 1), (4, 2), (3, 0)], ids=["skew1", "skew2", "col4"])
+def test_splat_bucket_edge_wraps(gpu, glass_scene, glass_oracle, splat_mode, bands, monkeypatch):
     """Edge-wrapped samples (x, y and the corner source with both) at their raster position in
     the tile pixels' sums: the skewed-time splat's flagged extra passes and the gather kernels'
     extra column / row, against the oracle's scatter, bit for bit."""
     import torch
+    if bands:
+        monkeypatch.setenv("NART_SKEW_BANDS", str(bands))
     p = _params(glass_scene, 32000, 32000, 16, bounces=1)
     ids = np.array(_edge_wrap_buckets(p), np.uint32)
     g = nart_amd.session_geometry(p)
