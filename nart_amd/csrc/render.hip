@@ -957,9 +957,9 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
     // for ~2/3 of the steps each): C5 1/2 shard 60 -> 49 ms (k_splat_col4: 62); a whole frame keeps
     // one band (C5 73 vs 92 ms with two).  Below 1 wave per SIMD k_splat_col4 is faster (C5 1/4,
     // 1/8 shards: 36 / 23 ms vs 41 / 37 with two bands; profiles/r03k_skew_band_ab.log).
-    // The two-band range is the volume integrator's only: the path kernels lose more to the
-    // pixel-major layout there than the splat gains (C3 1/2 shard: path kernels 196 -> 208 ms,
-    // splat 17 -> 13 ms; profiles/r03k_shard_scaling_c3.log).
+    // The two-band range is the volume integrator's only: for the path integrator the splat's
+    // gain at the C3 1/2 shard (17 -> 12.5 ms) is within the path kernels' run-to-run spread under
+    // the pixel-major layout (186-208 ms on one box; profiles/r03l_c3_half_shard_splat_ab.log).
     const double skew_from = p->integrator == NART_INTEGRATOR_VOLUME ? 0.5 * skew_min : skew_min;
     const int splat_mode = ctx->splat_mode >= 0 ? ctx->splat_mode : (skew_waves >= skew_from * 4.0 * n_cus ? 4 : 3);
     // NART_SKEW_BANDS (read per call): 1 or 2 forces the band count
