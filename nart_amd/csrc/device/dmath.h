@@ -8,6 +8,15 @@
 //  * sinf/cosf are glibc 2.35's algorithm (sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c,
 //    sincosf.h: double-precision range reduction + polynomials), verified bit-exact against
 //    the host libm over every float in [-7, 7] (tests/test_libm_parity.py).
+//
+// Third-party notices.  The sinf/cosf/logf ports restate algorithms and constant tables of the
+// GNU C Library 2.35 (sysdeps/ieee754/flt-32; those files are Copyright (C) 2017-2022 Free
+// Software Foundation, Inc. and Arm Ltd., licensed under the GNU Lesser General Public License
+// v2.1 or later).  The acosf/atanf/atan2f ports restate fdlibm's single-precision algorithms as
+// shipped in glibc ("Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+// Developed at SunPro, a Sun Microsystems, Inc. business.  Permission to use, copy, modify, and
+// distribute this software is freely granted, provided that this notice is preserved.").
+// They are needed to reproduce the reference's glm::sin/cos/acos/atan/log results bit for bit.
 #pragma once
 
 #include <hip/hip_runtime.h>
