@@ -891,7 +891,7 @@ int launch_latin(nart_ctx* ctx, const RenderArgs& ra, hipStream_t st) {
     const size_t stw = (size_t)((ra.n_slots + LATIN_EMIT_SLOTS - 1) / LATIN_EMIT_SLOTS) * LATIN_EMIT_SLOTS * ra.spp +
                        LATIN_ST_PAD;
     const bool three = ra.spp >= 2 && ra.spp <= 1024 && (4 * words + stw) * 4 <= ctx->cap_samples * sizeof(float4) &&
-                       (latin_env == 3 || (latin_env < 0 && ra.spp > 256));
+                       (latin_env == 3 || (latin_env < 0 && ra.spp > 64));  // C3 (256 spp): 6.7 -> 4.6 ms
     if (three) {
         uint32_t* base = reinterpret_cast<uint32_t*>(ra.Lout);
         ls.cx = base;
@@ -906,7 +906,7 @@ int launch_latin(nart_ctx* ctx, const RenderArgs& ra, hipStream_t st) {
         HIPCHK(hipGetLastError());
         return NART_OK;
     }
-    // (k_latin_idx at <= 256 spp measured slower: C3 11.0 vs 6.6 ms)
+    // (k_latin_idx at <= 256 spp measured slower: C3 11.0 vs 6.6 ms; the three-kernel form 4.6)
     if (ra.spp <= 256) {
         size_t lds = (size_t)ra.spp * 2 * 64 * sizeof(float);
         hipLaunchKernelGGL(k_latin_lds, dim3((ra.n_slots + 63) / 64), dim3(64), lds, st, ra);

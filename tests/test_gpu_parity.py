@@ -320,7 +320,7 @@ def test_octree_missed_camera_hit_samples(gpu, cornell_scene):
     assert _bits_equal(gs, rs), _report(gs, rs)
 
 
-@pytest.mark.parametrize("spp", [320, 512, 1024, 1040])
+@pytest.mark.parametrize("spp", [65, 100, 256, 320, 512, 1024, 1040])
 def test_latin_square_high_spp(gpu, glass_scene, glass_oracle, spp):
     """LatinSquare beyond the 256-spp LDS kernel: index shuffles in LDS with both arrays (<= 512
     spp) or one array per pass (<= 1024), and the global-memory kernel above that.  Per-sample
