@@ -209,12 +209,19 @@ def main():
     if rank == 0:
         image = torch.zeros((g.total_height, g.total_width, 5), dtype=torch.float32, device=dev)
 
+    ev = []  # per step: (start, rendered, gathered) events on the render stream
+
     def step(stats):
         nonlocal by_id
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e[0].record(stream)
         gpu.render_buckets_async(p, mine, shard.tiles.data_ptr(), stream.cuda_stream, stats)
+        e[1].record(stream)
         by_id = shard.gather()
+        e[2].record(stream)
         if rank == 0:
             gpu.combine_async(p, by_id.data_ptr(), image.data_ptr(), stream.cuda_stream)
+        ev.append(e)
 
     def barrier():
         torch.cuda.synchronize()
@@ -222,37 +229,57 @@ def main():
             import torch.distributed as td
             td.barrier()
 
-    # counter pass (not timed): algorithmic bytes per sample of this rank's buckets
-    cp = p.copy()
-    cp.spp = 16
-    gpu.set_counters(True)
-    cst = nart_amd.RenderStats()
-    ctiles = torch.zeros((len(mine), tpx, 5), dtype=torch.float32, device=dev)
-    gpu.render_buckets_async(cp, mine, ctiles.data_ptr(), stream.cuda_stream, cst)
-    gpu.set_counters(False)
-    counters = cst.as_dict()
-    del ctiles
+    # counter passes (not timed): algorithmic bytes per sample.  The figure priced in the roofline
+    # comes from the timed configuration itself (full spp) on the cpu_baseline bucket sample of this
+    # rank's share; a 16-spp pass over the whole share is reported beside it as a cross-check.
+    def counter_pass(ids, spp):
+        cp = p.copy()
+        cp.spp = spp
+        gpu.set_counters(True)
+        cst = nart_amd.RenderStats()
+        ctiles = torch.zeros((max(1, len(ids)), tpx, 5), dtype=torch.float32, device=dev)
+        gpu.render_buckets_async(cp, ids, ctiles.data_ptr(), stream.cuda_stream, cst)
+        torch.cuda.synchronize()
+        gpu.set_counters(False)
+        del ctiles
+        return cst.as_dict()
+
+    sample_ids, sample_stride = cpu_sample_ids(p, cfg["stride"])
+    mine_sample = np.intersect1d(mine, sample_ids).astype(np.uint32)
+    if len(mine_sample) == 0:
+        mine_sample = mine[:1]
+    counters = counter_pass(mine_sample, SPP)
+    counters16 = counter_pass(mine, min(16, SPP))
 
     for _ in range(a.warmup):
         step(nart_amd.RenderStats())
     barrier()
+    ev.clear()
     st = nart_amd.RenderStats()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step(st)
     barrier()
     dt = time.perf_counter() - t0
+    render_ms = [e[0].elapsed_time(e[1]) for e in ev]
+    gather_ms = [e[1].elapsed_time(e[2]) for e in ev]
+    mine_t = torch.tensor([dt, sum(render_ms) / len(ev), sum(gather_ms) / len(ev)], dtype=torch.float64)
+    per_rank = [mine_t]
     if dist:
         import torch.distributed as td
         tt = torch.tensor([dt], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         td.all_reduce(tt, op=td.ReduceOp.MAX)
         dt = float(tt.item())
+        src = mine_t.to(dev) if backend == "nccl" else mine_t
+        per_rank = [torch.zeros_like(src) for _ in range(world)]
+        td.all_gather(per_rank, src)
 
     samples_total = W * H * SPP * a.steps
     value = samples_total / dt / 1e6
     kernel_avg_ms = st.kernel_ms / max(1, st.kernel_launches)  # k_primary + k_render_rq per launch
     primary_avg_ms = st.primary_ms / max(1, st.kernel_launches)
     bps = bytes_per_sample(counters)
+    bps16 = bytes_per_sample(counters16)
     per_launch_samples = st.traced_samples / max(1, st.kernel_launches)
     achieved = bps * per_launch_samples / (kernel_avg_ms * 1e-3) / 1e9
     prof, prof_src = load_profile("%dx%dx%d" % (W, H, SPP))
@@ -275,6 +302,11 @@ def main():
                 "traffic_source": prof_src,
                 "kernel": "k_render_volume_sm" if p.integrator == 1 else "k_primary + k_render_rq",
                 "kernel_avg_ms": round(kernel_avg_ms, 3), "bytes_per_sample": round(bps, 1),
+                "bytes_per_sample_source": {
+                    "spp": SPP, "sample": "counter pass at the timed spp over %d buckets of this rank's share (the "
+                                          "cpu_baseline sample: every %dth bucket)" % (len(mine_sample), sample_stride),
+                    "cross_check_16spp_whole_share": round(bps16, 1),
+                    "ratio_16spp_over_timed": round(bps16 / bps, 4)},
                 "rays_per_s": round((counters["rays_extend"] + counters["rays_shadow"]) /
                                     max(1, counters["traced_samples"]) * per_launch_samples /
                                     (kernel_avg_ms * 1e-3), 1)}
@@ -311,6 +343,9 @@ def main():
             "splat_ms_per_step": round(st.splat_ms / a.steps, 3),
             "latin_ms_per_step": round(st.latin_ms / a.steps, 3),
             "image_finite": img_ok,
+            "per_rank_ms": [{"rank": r, "step_wall_ms": round(float(v[0]) / a.steps * 1e3, 3),
+                             "render_ms": round(float(v[1]), 3), "gather_ms": round(float(v[2]), 3)}
+                            for r, v in enumerate(t.cpu() for t in per_rank)],
             "counters_per_sample": {k: round(counters[k] / max(1, counters["traced_samples"]), 3)
                                     for k in ("rays_extend", "rays_shadow", "node_visits", "tri_tests",
                                               "bounces", "octree_checks", "octree_replays")},

@@ -60,11 +60,22 @@ const char* nart_hip_last_error(const nart_ctx* ctx);
    xGMI) and combines them there in bucket raster order (render.cpp:183-203), so the image is
    bit-identical for any n.  n_devices == 1 is exactly nart_hip_create.  Repeated ordinals (a
    rehearsal of n devices on fewer GPUs) gather with device copies, since RCCL needs distinct
-   GPUs; NART_GATHER=rccl|copy overrides.  NART_E_RCCL if the communicator cannot be built. */
+   GPUs; NART_GATHER=rccl|copy overrides (read at creation).  If librccl cannot be loaded or
+   ncclCommInitAll fails, the context falls back to the device-copy gather (same image;
+   nart_hip_context_devices reports it); only NART_GATHER=rccl then fails with NART_E_RCCL.
+   A gather that fails inside the RCCL group still closes the group (ncclGroupEnd), returns
+   NART_E_RCCL and marks the context unusable: every later render returns NART_E_RCCL, and the
+   caller destroys the context and creates a new one. */
 int nart_hip_create_multi(const nart_scene_blob* scene, const int* device_ids, int n_devices, nart_ctx** out);
 
-/* Devices of a context (1 for nart_hip_create) and whether its gather runs over RCCL. */
+/* Devices of a context (1 for nart_hip_create) and its gather: uses_rccl = 1 RCCL, 0 device
+   copies, 2 device copies because RCCL was unavailable (the fallback above). */
 int nart_hip_context_devices(const nart_ctx* ctx, int* n_devices, int* uses_rccl);
+
+/* Test hook (no reference counterpart): fault 1 makes the next RCCL gather of a multi-device
+   context post a send to a rank that does not exist, exercising the failure path above; 0 clears.
+   No effect on device-copy gathers. */
+int nart_hip_debug_fault(nart_ctx* ctx, int fault);
 
 /* HIP devices visible to this process. */
 int nart_hip_device_count(int* count);

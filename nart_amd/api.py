@@ -125,6 +125,7 @@ _HIP_SIGS = {
     "nart_hip_bvh_info": (ctypes.c_int, [_P, ctypes.POINTER(BvhInfo)]),
     "nart_hip_create_multi": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(_P)]),
     "nart_hip_context_devices": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "nart_hip_debug_fault": (ctypes.c_int, [_P, ctypes.c_int]),
     "nart_hip_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "nart_hip_context_bvh": (ctypes.c_int, [_P, ctypes.POINTER(BvhInfo), ctypes.POINTER(ctypes.c_double)]),
     "nart_hip_shard_buckets": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -358,7 +359,17 @@ class HipRenderer:
         """(number of devices, gather over RCCL) of this context."""
         n, r = ctypes.c_int(), ctypes.c_int()
         self._check(self._lib.nart_hip_context_devices(self._ctx, ctypes.byref(n), ctypes.byref(r)))
-        return n.value, bool(r.value)
+        return n.value, r.value == 1
+
+    def gather_mode(self):
+        """"rccl", "copy", or "copy-fallback" (RCCL requested implicitly but unavailable)."""
+        n, r = ctypes.c_int(), ctypes.c_int()
+        self._check(self._lib.nart_hip_context_devices(self._ctx, ctypes.byref(n), ctypes.byref(r)))
+        return {1: "rccl", 0: "copy", 2: "copy-fallback"}[r.value]
+
+    def debug_fault(self, fault):
+        """Test hook (nart_hip_debug_fault): 1 = the next RCCL gather posts an invalid peer."""
+        self._check(self._lib.nart_hip_debug_fault(self._ctx, int(fault)))
 
     def set_counters(self, on):
         self._check(self._lib.nart_hip_set_counters(self._ctx, 1 if on else 0))

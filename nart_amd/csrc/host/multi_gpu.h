@@ -65,12 +65,6 @@ const RcclApi& rccl_api() {
     return api;
 }
 
-#define RCCLCHK(call)                                                                              \
-    do {                                                                                           \
-        ncclResult_t r_ = (call);                                                                  \
-        if (r_ != ncclSuccess) return fail(ctx, NART_E_RCCL, std::string(#call ": ") + R.ErrStr(r_)); \
-    } while (0)
-
 // Bucket ids of device d out of n (bucket b -> device b % n), in ascending order.
 std::vector<uint32_t> shard_ids(uint32_t n_buckets, uint32_t n, uint32_t d) {
     std::vector<uint32_t> ids;
@@ -91,13 +85,15 @@ __global__ void k_unshard(const float* slabs, float* by_id, uint32_t n_buckets, 
     for (uint32_t k = threadIdx.x; k < tile_floats; k += blockDim.x) dst[k] = src[k];
 }
 
+// One render's device statistics: device times of the slowest device (the devices run
+// concurrently), work counts summed.  The caller adds the result to its own stats, as the
+// single-device path does (a stats struct reused over renders keeps accumulating).
 void merge_stats(nart_render_stats& out, const nart_render_stats& s) {
-    // device times: the slowest device (the devices run concurrently); work counts: summed
     out.kernel_ms = std::max(out.kernel_ms, s.kernel_ms);
     out.splat_ms = std::max(out.splat_ms, s.splat_ms);
     out.latin_ms = std::max(out.latin_ms, s.latin_ms);
     out.primary_ms = std::max(out.primary_ms, s.primary_ms);
-    out.kernel_launches += s.kernel_launches;
+    out.kernel_launches = std::max(out.kernel_launches, s.kernel_launches);
     out.samples += s.samples;
     out.traced_samples += s.traced_samples;
     out.rays_extend += s.rays_extend;
@@ -123,6 +119,8 @@ int ensure_dev(nart_ctx* ctx, int dev, void*& buf, size_t& cap, size_t bytes, co
 // Render(), multi-device: shard, render concurrently, gather to device 0, combine, copy out.
 int render_multi(nart_ctx* ctx, const nart_render_params* p, nart_pixel* image, nart_render_stats* stats) {
     const uint32_t n = (uint32_t)ctx->subs.size();
+    if (ctx->rccl_broken)
+        return fail(ctx, NART_E_RCCL, "an earlier RCCL gather of this context failed; destroy it and create a new one");
     int rc = check_params(ctx->subs[0], p);
     if (rc) return fail(ctx, rc, ctx->subs[0]->err);
     nart_session_geometry g;
@@ -147,18 +145,24 @@ int render_multi(nart_ctx* ctx, const nart_render_params* p, nart_pixel* image, 
     std::vector<int> rcs(n, NART_OK);
     std::vector<nart_render_stats> st(n);
     std::vector<std::thread> th;
-    for (uint32_t d = 0; d < n; ++d) {
-        std::memset(&st[d], 0, sizeof(st[d]));
-        th.emplace_back([&, d] {
-            if (ids[d].empty()) return;
-            if (hipSetDevice(ctx->devs[d]) != hipSuccess) {
-                rcs[d] = NART_E_HIP;
-                return;
-            }
-            rcs[d] = render_buckets(ctx->subs[d], p, ids[d].data(), (uint32_t)ids[d].size(),
-                                    static_cast<float*>(ctx->sub_tiles[d]), ctx->streams[d], &st[d]);
-            if (rcs[d] == NART_OK && hipStreamSynchronize(ctx->streams[d]) != hipSuccess) rcs[d] = NART_E_HIP;
-        });
+    auto work = [&](uint32_t d) {
+        if (ids[d].empty()) return;
+        if (hipSetDevice(ctx->devs[d]) != hipSuccess) {
+            rcs[d] = NART_E_HIP;
+            return;
+        }
+        rcs[d] = render_buckets(ctx->subs[d], p, ids[d].data(), (uint32_t)ids[d].size(),
+                                static_cast<float*>(ctx->sub_tiles[d]), ctx->streams[d], &st[d]);
+        if (rcs[d] == NART_OK && hipStreamSynchronize(ctx->streams[d]) != hipSuccess) rcs[d] = NART_E_HIP;
+    };
+    for (uint32_t d = 0; d < n; ++d) std::memset(&st[d], 0, sizeof(st[d]));
+    try {
+        th.reserve(n);
+        for (uint32_t d = 0; d < n; ++d) th.emplace_back(work, d);
+    } catch (...) {
+        // no thread (or no room for one): join the ones started, report; nothing escapes the ABI
+        for (auto& t : th) t.join();
+        return fail(ctx, NART_E_OOM, "cannot start the per-device render threads");
     }
     for (auto& t : th) t.join();
     for (uint32_t d = 0; d < n; ++d)
@@ -166,20 +170,47 @@ int render_multi(nart_ctx* ctx, const nart_render_params* p, nart_pixel* image, 
             return fail(ctx, rcs[d], "device " + std::to_string(ctx->devs[d]) + ": " + ctx->subs[d]->err);
 
     // 2. gather the slabs to device 0 (rank order), RCCL over xGMI or device copies
-    std::vector<size_t> first(n, 0);
-    for (uint32_t d = 1; d < n; ++d) first[d] = first[d - 1] + ids[d - 1].size();
+    std::vector<size_t> first_b(n, 0);
+    for (uint32_t d = 1; d < n; ++d) first_b[d] = first_b[d - 1] + ids[d - 1].size();
     float* slabs = static_cast<float*>(ctx->d_gather);
     hipStream_t s0 = ctx->streams[0];
     if (ctx->gather_rccl) {
+        // every error inside the group is recorded and the group is always closed (an open group
+        // would capture the next render's calls); a failed gather leaves the communicator in an
+        // unknown state, so the context refuses further renders (rccl_broken)
         const RcclApi& R = rccl_api();
-        RCCLCHK(R.GroupStart());
-        for (uint32_t d = 0; d < n; ++d) {
-            if (ids[d].empty()) continue;
-            const size_t cnt = ids[d].size() * tile_floats;
-            RCCLCHK(R.Send(ctx->sub_tiles[d], cnt, ncclFloat32, 0, ctx->comms[d], ctx->streams[d]));
-            RCCLCHK(R.Recv(slabs + first[d] * tile_floats, cnt, ncclFloat32, (int)d, ctx->comms[0], s0));
+        ncclResult_t first = ncclSuccess;
+        std::string where;
+        auto note = [&](ncclResult_t r, const char* what) {
+            if (r != ncclSuccess && first == ncclSuccess) {
+                first = r;
+                where = what;
+            }
+        };
+        note(R.GroupStart(), "ncclGroupStart");
+        if (first == ncclSuccess) {
+            // test hook (nart_hip_debug_fault 1): the last device sends to a rank that does not exist
+            const int bad_peer = ctx->debug_fault == 1 ? (int)n : 0;
+            for (uint32_t d = 0; d < n; ++d) {
+                if (ids[d].empty()) continue;
+                const size_t cnt = ids[d].size() * tile_floats;
+                note(R.Send(ctx->sub_tiles[d], cnt, ncclFloat32, d + 1 == n ? bad_peer : 0, ctx->comms[d], ctx->streams[d]),
+                     "ncclSend");
+                note(R.Recv(slabs + first_b[d] * tile_floats, cnt, ncclFloat32, (int)d, ctx->comms[0], s0), "ncclRecv");
+            }
+            note(R.GroupEnd(), "ncclGroupEnd");
         }
-        RCCLCHK(R.GroupEnd());
+        ctx->debug_fault = 0;
+        if (first != ncclSuccess) {
+            ctx->rccl_broken = true;
+            for (uint32_t d = 0; d < n; ++d) {
+                hipSetDevice(ctx->devs[d]);
+                hipStreamSynchronize(ctx->streams[d]);
+            }
+            (void)hipGetLastError();
+            return fail(ctx, NART_E_RCCL, where + ": " + R.ErrStr(first) +
+                                              " (context unusable: destroy it and create a new one)");
+        }
         for (uint32_t d = 1; d < n; ++d) {
             HIPCHK(hipSetDevice(ctx->devs[d]));
             HIPCHK(hipStreamSynchronize(ctx->streams[d]));
@@ -189,7 +220,7 @@ int render_multi(nart_ctx* ctx, const nart_render_params* p, nart_pixel* image, 
         HIPCHK(hipSetDevice(dev0));
         for (uint32_t d = 0; d < n; ++d)
             if (!ids[d].empty())
-                HIPCHK(hipMemcpyPeerAsync(slabs + first[d] * tile_floats, dev0, ctx->sub_tiles[d], ctx->devs[d],
+                HIPCHK(hipMemcpyPeerAsync(slabs + first_b[d] * tile_floats, dev0, ctx->sub_tiles[d], ctx->devs[d],
                                           ids[d].size() * tile_floats * 4, s0));
     }
 
@@ -202,8 +233,25 @@ int render_multi(nart_ctx* ctx, const nart_render_params* p, nart_pixel* image, 
         return fail(ctx, rc, ctx->subs[0]->err);
     HIPCHK(hipMemcpyAsync(image, ctx->d_image, img_bytes, hipMemcpyDeviceToHost, s0));
     HIPCHK(hipStreamSynchronize(s0));
-    if (stats)
-        for (uint32_t d = 0; d < n; ++d) merge_stats(*stats, st[d]);
+    if (stats) {
+        nart_render_stats m;
+        std::memset(&m, 0, sizeof(m));
+        for (uint32_t d = 0; d < n; ++d) merge_stats(m, st[d]);
+        stats->kernel_ms += m.kernel_ms;
+        stats->splat_ms += m.splat_ms;
+        stats->latin_ms += m.latin_ms;
+        stats->primary_ms += m.primary_ms;
+        stats->kernel_launches += m.kernel_launches;
+        stats->samples += m.samples;
+        stats->traced_samples += m.traced_samples;
+        stats->rays_extend += m.rays_extend;
+        stats->rays_shadow += m.rays_shadow;
+        stats->node_visits += m.node_visits;
+        stats->tri_tests += m.tri_tests;
+        stats->bounces += m.bounces;
+        stats->octree_checks += m.octree_checks;
+        stats->octree_replays += m.octree_replays;
+    }
     return NART_OK;
 }
 

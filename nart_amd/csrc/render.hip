@@ -88,6 +88,13 @@ struct nart_ctx {
     std::vector<size_t> sub_cap;
     std::vector<ncclComm_t> comms;
     bool gather_rccl = false;
+    // RCCL requested implicitly (distinct devices) but unavailable: device-copy gather instead
+    bool gather_fallback = false;
+    // an RCCL gather failed: the communicator's state is unknown, every later render of this
+    // context returns NART_E_RCCL (destroy it and create a new one)
+    bool rccl_broken = false;
+    int debug_fault = 0;     // nart_hip_debug_fault (tests only)
+    uint32_t mem_share = 1;  // contexts of one multi-device context sharing this device ordinal
     // acceleration structure: built on the device (NART_BVH_BUILD=device) or the host; build time
     bool bvh_on_device = false;
     double bvh_ms = 0.0;
@@ -296,6 +303,9 @@ size_t batch_slot_limit(const nart_ctx* ctx, uint32_t spp) {
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
         const size_t held = ctx->cap_samples * (sizeof(float2) + sizeof(float4) + sizeof(uint32_t));
         budget = std::max(budget, (free_b + held) / 2);
+        // sub-contexts that share an ordinal (a multi-device rehearsal) render concurrently and
+        // each sees the same free memory: split the budget between them
+        budget /= std::max<uint32_t>(1, ctx->mem_share);
     } else {
         (void)hipGetLastError();
     }
@@ -1879,20 +1889,29 @@ int nart_hip_create_multi(const nart_scene_blob* blob, const int* device_ids, in
             return bail(NART_E_HIP);
         ctx->streams.push_back(st);
     }
+    for (int d = 0; d < n_devices; ++d)
+        for (int j = 0; j < n_devices; ++j) ctx->subs[d]->mem_share += (j != d && device_ids[j] == device_ids[d]) ? 1u : 0u;
     ctx->gather_rccl = force_rccl || (distinct && !force_copy);
     if (ctx->gather_rccl) {
         const RcclApi& R = rccl_api();
-        if (!R.ok || !distinct) {
-            const int rc = NART_E_RCCL;
-            nart_hip_destroy(ctx);
-            return rc;
+        bool ok = R.ok && distinct;
+        if (ok) {
+            ctx->comms.assign(n_devices, nullptr);
+            if (R.CommInitAll(ctx->comms.data(), n_devices, device_ids) != ncclSuccess) {
+                ctx->comms.clear();
+                (void)hipGetLastError();
+                ok = false;
+            }
         }
-        ctx->comms.assign(n_devices, nullptr);
-        if (R.CommInitAll(ctx->comms.data(), n_devices, device_ids) != ncclSuccess) {
-            ctx->comms.clear();
-            return bail(NART_E_RCCL);
+        if (!ok) {
+            // NART_GATHER=rccl demands RCCL; otherwise the device-copy gather serves the same
+            // image (nart_hip_context_devices reports the fallback)
+            if (force_rccl) return bail(NART_E_RCCL);
+            ctx->gather_rccl = false;
+            ctx->gather_fallback = true;
         }
-    } else {
+    }
+    if (!ctx->gather_rccl) {
         // device copies to device 0 (peer access where the devices differ)
         hipSetDevice(device_ids[0]);
         for (int d = 1; d < n_devices; ++d)
@@ -1910,7 +1929,13 @@ int nart_hip_create_multi(const nart_scene_blob* blob, const int* device_ids, in
 int nart_hip_context_devices(const nart_ctx* ctx, int* n_devices, int* uses_rccl) {
     if (!ctx || !n_devices) return NART_E_INVALID;
     *n_devices = ctx->subs.empty() ? 1 : (int)ctx->subs.size();
-    if (uses_rccl) *uses_rccl = ctx->gather_rccl ? 1 : 0;
+    if (uses_rccl) *uses_rccl = ctx->gather_rccl ? 1 : (ctx->gather_fallback ? 2 : 0);
+    return NART_OK;
+}
+
+int nart_hip_debug_fault(nart_ctx* ctx, int fault) {
+    if (!ctx || fault < 0 || fault > 1) return NART_E_INVALID;
+    ctx->debug_fault = fault;
     return NART_OK;
 }
 

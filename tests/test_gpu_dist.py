@@ -86,6 +86,10 @@ def test_bench_spawned_ranks_on_one_gpu(gpu, glass_scene, tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 2
+    ranks = line["per_rank_ms"]
+    assert [r["rank"] for r in ranks] == [0, 1]
+    assert all(r["render_ms"] > 0 and r["gather_ms"] >= 0 for r in ranks)
+    assert line["roofline"]["bytes_per_sample_source"]["spp"] == 8
     img = np.load(out)
     p = nart_amd.load_sessions(glass_scene.path)[0]
     p.image_width, p.image_height, p.spp = 200, 120, 8

@@ -70,3 +70,35 @@ def test_multi_device_rejects_bucket_api(gpu, glass_scene):
     with pytest.raises(nart_amd.NartError) as e:
         m.render_buckets_async(p, np.arange(4, dtype=np.uint32), t.data_ptr())
     assert e.value.code == -6  # NART_E_UNSUPPORTED: one context per rank for the bucket API
+
+
+def test_rccl_gather_failure_marks_context(gpu, glass_scene, monkeypatch):
+    """A gather that fails inside the RCCL group (test hook: a send to a rank that does not exist)
+    closes the group, returns NART_E_RCCL and leaves the context refusing further renders; a fresh
+    context then renders bit-identically (render.cpp:152-203 contract)."""
+    monkeypatch.setenv("NART_GATHER", "rccl")
+    p = _params(glass_scene, 64, 48, 4)
+    m = nart_amd.HipRenderer(glass_scene, devices=[0])
+    assert m.gather_mode() == "rccl"
+    m.debug_fault(1)
+    with pytest.raises(nart_amd.NartError) as e:
+        m.render(p)
+    assert e.value.code == -5  # NART_E_RCCL
+    with pytest.raises(nart_amd.NartError) as e2:
+        m.render(p)
+    assert e2.value.code == -5 and "destroy" in str(e2.value)
+    m.close()
+    fresh = nart_amd.HipRenderer(glass_scene, devices=[0])
+    assert _bits_equal(fresh.render(p), oracle.Oracle(glass_scene).render(p))
+
+
+def test_multi_device_stats_accumulate(gpu, glass_scene):
+    """A stats struct reused over renders keeps accumulating on a multi-device context, as on one
+    device (device times of the slowest device per render, added up)."""
+    p = _params(glass_scene, 64, 48, 2)
+    m = nart_amd.HipRenderer(glass_scene, devices=[0, 0])
+    st = nart_amd.RenderStats()
+    m.render(p, st)
+    k1, s1 = st.kernel_ms, st.traced_samples
+    m.render(p, st)
+    assert st.kernel_ms > k1 and st.traced_samples == 2 * s1

@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--ns", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("-s", type=int, default=0)
     ap.add_argument("--reps", type=int, default=2)
-    ap.add_argument("--rank", type=int, default=-1, help="-1: every rank of each N (max reported)")
+    ap.add_argument("--rank", type=int, default=-1, help="-1: every rank of each N (all reported, worst and spread)")
     ap.add_argument("--config", default="c3", help="bench.py config (c2, c3, c4, c5); -s overrides its spp")
     a = ap.parse_args()
     sys.path.insert(0, REPO)
@@ -61,12 +61,13 @@ def main():
                     best = d
             best["rank"] = r
             per.append(best)
-            if n >= 4 and a.rank < 0 and r >= 1:
-                break  # ranks of one N are statistically alike; two suffice
         worst = max(per, key=lambda d: d["wall_ms"])
+        walls = [d["wall_ms"] for d in per]
         print(json.dumps({"n": n, "buckets_per_rank": len(BucketShard(nb, tpx, 0, n, "cpu").mine),
                           "worst": {k: round(v, 3) for k, v in worst.items()},
-                          "ideal_wall_ms": None}), flush=True)
+                          "spread": {"min_ms": round(min(walls), 3), "max_ms": round(max(walls), 3),
+                                     "mean_ms": round(sum(walls) / len(walls), 3)},
+                          "ranks": [{k: round(v, 3) for k, v in d.items()} for d in per]}), flush=True)
 
 
 if __name__ == "__main__":
