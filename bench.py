@@ -203,7 +203,7 @@ def main():
     gpu = nart_amd.HipRenderer(scene, device=local)
     stream = torch.cuda.current_stream()
     dev = torch.device("cuda", local)
-    shard = BucketShard(nb, tpx, rank, world, dev)  # interleaved buckets, gather to rank 0
+    shard = BucketShard(g.n_buckets_x, nb, tpx, rank, world, dev)  # interleaved buckets, gather to rank 0
     mine = shard.mine
     by_id = None
     if rank == 0:

@@ -54,7 +54,7 @@ const char* nart_hip_last_error(const nart_ctx* ctx);
 
 /* Multi-GPU context over device_ids[0..n_devices) of this node, replacing the reference's
    tbb::task_group over host cores (render.cpp:152-177): the scene is uploaded to every device;
-   nart_hip_render shards the buckets (bucket b -> device b % n, nart_hip_shard_buckets), renders
+   nart_hip_render shards the buckets (dealt in a low-discrepancy order, nart_hip_shard_buckets), renders
    the shares concurrently (one host thread per device), gathers the tiles to device_ids[0] with
    the library's own RCCL communicator (ncclCommInitAll over the list; ncclSend/ncclRecv over
    xGMI) and combines them there in bucket raster order (render.cpp:183-203), so the image is
@@ -80,10 +80,12 @@ int nart_hip_debug_fault(nart_ctx* ctx, int fault);
 /* HIP devices visible to this process. */
 int nart_hip_device_count(int* count);
 
-/* Host only: the buckets device device_index of n_devices renders (ascending ids b with
-   b % n_devices == device_index) into ids (may be null to query the count). */
-int nart_hip_shard_buckets(uint32_t n_buckets, uint32_t n_devices, uint32_t device_index, uint32_t* ids,
-                           uint32_t* count);
+/* Host only: the buckets device device_index of n_devices renders, ascending, into ids (may be
+   null to query the count).  A diagonal lattice: bucket id b = by*n_buckets_x + bx goes to device
+   (bx + s*by) % n_devices, s the step in [1, n) coprime to n closest to 0.382 n (3 for 8 devices),
+   so every region of the frame splits evenly over the devices (nart_amd/dist.py bucket_owners). */
+int nart_hip_shard_buckets(uint32_t n_buckets_x, uint32_t n_buckets, uint32_t n_devices, uint32_t device_index,
+                           uint32_t* ids, uint32_t* count);
 
 /* Whole-session render, Render()-equivalent: fills a caller-owned host buffer of
    totalW*totalH nart_pixel (render.cpp:114-206 contract, render.h:18-21 layout). */

@@ -128,7 +128,7 @@ _HIP_SIGS = {
     "nart_hip_debug_fault": (ctypes.c_int, [_P, ctypes.c_int]),
     "nart_hip_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "nart_hip_context_bvh": (ctypes.c_int, [_P, ctypes.POINTER(BvhInfo), ctypes.POINTER(ctypes.c_double)]),
-    "nart_hip_shard_buckets": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+    "nart_hip_shard_buckets": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                               ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
 }
 SCENE_SYMBOLS = tuple(_SCENE_SIGS)
@@ -298,15 +298,16 @@ class Scene:
             pass
 
 
-def shard_buckets(n_buckets, n_devices, device_index):
-    """Host only: the bucket ids a multi-device context renders on device_index (b % n == index)."""
+def shard_buckets(n_buckets_x, n_buckets, n_devices, device_index):
+    """Host only: the bucket ids a multi-device context renders on device_index (diagonal lattice,
+    nart_hip_shard_buckets; the same partition as nart_amd.dist.bucket_owners)."""
     lib = hip_lib()
     cnt = ctypes.c_uint32()
-    rc = lib.nart_hip_shard_buckets(n_buckets, n_devices, device_index, None, ctypes.byref(cnt))
+    rc = lib.nart_hip_shard_buckets(n_buckets_x, n_buckets, n_devices, device_index, None, ctypes.byref(cnt))
     if rc != NART_OK:
         raise NartError(rc, "nart_hip_shard_buckets")
     ids = np.zeros(max(1, cnt.value), np.uint32)
-    lib.nart_hip_shard_buckets(n_buckets, n_devices, device_index,
+    lib.nart_hip_shard_buckets(n_buckets_x, n_buckets, n_devices, device_index,
                                ids.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(cnt))
     return ids[:cnt.value]
 

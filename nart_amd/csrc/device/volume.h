@@ -264,14 +264,26 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
     }
     __syncthreads();
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= A.n_slots) return;
-    const uint32_t slot = A.queue ? A.queue[gid] : gid;
-    const uint32_t xy = A.slot_xy[slot];
-    const uint32_t px = xy & 0xFFFFu, py = xy >> 16;
-    uint32_t rng = A.rng0[slot];
-    const SlotSO so = A.slot_so[slot];
-    const float2* smp = A.samples + so.first;
-    float4* out = A.Lout + so.first;
+    // with A.qhead the grid is persistent: a lane whose pixel is done takes the next queue entry
+    // (queue[qbase + atomicAdd(qhead)]) instead of idling until its wave ends
+    const uint32_t qlen = A.qlen ? A.qlen : A.n_slots;
+    if (gid >= (A.qhead ? qlen : A.n_slots)) return;
+    uint32_t slot = A.queue ? A.queue[gid] : gid;
+    uint32_t px = 0, py = 0, rng = 0;
+    SlotSO so;
+    const float2* smp = nullptr;
+    float4* out = nullptr;
+    auto take = [&](uint32_t sl) {
+        slot = sl;
+        const uint32_t xy = A.slot_xy[sl];
+        px = xy & 0xFFFFu;
+        py = xy >> 16;
+        rng = A.rng0[sl];
+        so = A.slot_so[sl];
+        smp = A.samples + so.first;
+        out = A.Lout + so.first;
+    };
+    take(slot);
     const DMedium& m = S.medium;
     const f3 beta = F3(1.f, 1.f, 1.f);
     enum { P_SAMPLE, P_RAY, P_MAJ, P_COLL, P_ESC };
@@ -283,7 +295,13 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
     for (;;) {
         bool finish = false;
         if (ph == P_SAMPLE) {
-            if (s >= A.spp) break;
+            if (s >= A.spp) {
+                if (!A.qhead || A.cost) break;
+                const uint32_t idx = A.qbase + atomicAdd(A.qhead, 1u);
+                if (idx >= qlen) break;
+                take(A.queue[idx]);
+                s = 0;
+            }
             const float2 sm = smp[(size_t)s * so.stride];
             const Ray r = cast_ray(S, F2(sm.x, sm.y), A.W, A.H, px, py);
             o = r.o;

@@ -7,6 +7,29 @@
 // 16-bit words of every channel plane, wavelet-transformed per plane.  Decoding reverses the
 // Huffman code, the 2D Haar-like wavelet (14- or 16-bit variant by the value range), maps
 // values back through the bitmap's reverse LUT and interleaves planes into scanlines.
+//
+// Third-party notice.  The Huffman decoder (code-length unpacking with the zero-run codes, the
+// canonical code table, the decoding table) and the wavelet decoder restate OpenEXR's
+// ImfHuf.cpp and ImfWav.cpp, whose constants and structure they keep:
+//   Copyright (c) 2002-2012, Industrial Light & Magic, a division of Lucas Digital Ltd. LLC.
+//   Copyright (c) Contributors to the OpenEXR Project.  All rights reserved.
+//   SPDX-License-Identifier: BSD-3-Clause.
+//   Redistribution and use in source and binary forms, with or without modification, are
+//   permitted provided that the following conditions are met: (1) redistributions of source code
+//   must retain the above copyright notice, this list of conditions and the following disclaimer;
+//   (2) redistributions in binary form must reproduce the above copyright notice, this list of
+//   conditions and the following disclaimer in the documentation and/or other materials provided
+//   with the distribution; (3) neither the name of the copyright holder nor the names of its
+//   contributors may be used to endorse or promote products derived from this software without
+//   specific prior written permission.  THIS SOFTWARE IS PROVIDED BY THE COPYRIGHT HOLDERS AND
+//   CONTRIBUTORS "AS IS" AND ANY EXPRESS OR IMPLIED WARRANTIES, INCLUDING, BUT NOT LIMITED TO, THE
+//   IMPLIED WARRANTIES OF MERCHANTABILITY AND FITNESS FOR A PARTICULAR PURPOSE ARE DISCLAIMED. IN NO
+//   EVENT SHALL THE COPYRIGHT HOLDER OR CONTRIBUTORS BE LIABLE FOR ANY DIRECT, INDIRECT,
+//   INCIDENTAL, SPECIAL, EXEMPLARY, OR CONSEQUENTIAL DAMAGES (INCLUDING, BUT NOT LIMITED TO,
+//   PROCUREMENT OF SUBSTITUTE GOODS OR SERVICES; LOSS OF USE, DATA, OR PROFITS; OR BUSINESS
+//   INTERRUPTION) HOWEVER CAUSED AND ON ANY THEORY OF LIABILITY, WHETHER IN CONTRACT, STRICT
+//   LIABILITY, OR TORT (INCLUDING NEGLIGENCE OR OTHERWISE) ARISING IN ANY WAY OUT OF THE USE OF
+//   THIS SOFTWARE, EVEN IF ADVISED OF THE POSSIBILITY OF SUCH DAMAGE.
 #include "exr_piz.h"
 
 #include <cstring>

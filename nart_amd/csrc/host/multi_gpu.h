@@ -4,8 +4,8 @@
 // their tiles into the image in bucket raster order (render.cpp:152-203).  Here one process drives
 // N GPUs of the node:
 //   * the scene lives on every device (one single-device sub-context each, nart_hip_create);
-//   * bucket b belongs to device b % N (interleaved, so the costly regions of a frame spread over
-//     all devices; nart_hip_shard_buckets);
+//   * buckets are dealt over the devices on a diagonal lattice (shard_ids: every region of a frame
+//     spreads evenly over all devices; nart_hip_shard_buckets);
 //   * one host thread per device renders its share into device-resident tiles (render_buckets);
 //   * the tiles are gathered to device 0 with one RCCL group of ncclSend / ncclRecv over xGMI
 //     (library-owned communicator, ncclCommInitAll over the device list), permuted into bucket-id
@@ -65,23 +65,46 @@ const RcclApi& rccl_api() {
     return api;
 }
 
-// Bucket ids of device d out of n (bucket b -> device b % n), in ascending order.
-std::vector<uint32_t> shard_ids(uint32_t n_buckets, uint32_t n, uint32_t d) {
+// Bucket ids of device d out of n, in ascending order: a diagonal lattice, bucket (bx, by) on
+// device (bx + s*by) % n with s = lattice_step(n), the s in [1, n) coprime to n closest to 0.382 n.
+// Every run of n buckets along a row or a column holds each device once, so every region of the
+// frame -- the costly glass of C3 -- splits evenly over the devices.  (b % n gave whole vertical
+// stripes when n divides the bucket-column count: C3 1/8 shards 86-101 ms.)  Must match
+// nart_amd/dist.py bucket_owners.
+uint32_t lattice_step(uint32_t n) {
+    uint32_t best = 0;
+    double bd = 1e30;
+    for (uint32_t s = 1; s < n; ++s) {
+        uint32_t a = s, b = n;
+        while (b) {
+            const uint32_t t = a % b;
+            a = b;
+            b = t;
+        }
+        const double dd = std::fabs((double)s - 0.382 * (double)n);
+        if (a == 1 && dd < bd) {
+            bd = dd;
+            best = s;
+        }
+    }
+    return best;
+}
+
+std::vector<uint32_t> shard_ids(uint32_t nbx, uint32_t n_buckets, uint32_t n, uint32_t d) {
     std::vector<uint32_t> ids;
-    for (uint32_t b = d; b < n_buckets; b += n) ids.push_back(b);
+    const uint32_t s = lattice_step(n);
+    for (uint32_t b = 0; b < n_buckets; ++b)
+        if ((uint32_t)(((uint64_t)(b % nbx) + (uint64_t)s * (b / nbx)) % n) == d) ids.push_back(b);
     return ids;
 }
 
-// Gathered slabs (device d's tiles at slab_first(d), its i-th bucket being id d + i*n) -> tiles in
-// bucket-id order.  One block per bucket.
-__global__ void k_unshard(const float* slabs, float* by_id, uint32_t n_buckets, uint32_t n, uint32_t tile_floats) {
-    const uint32_t b = blockIdx.x;
-    if (b >= n_buckets) return;
-    const uint32_t d = b % n, i = b / n;
-    uint32_t first = 0;
-    for (uint32_t q = 0; q < d; ++q) first += (n_buckets - q + n - 1) / n;
-    const float* src = slabs + (size_t)(first + i) * tile_floats;
-    float* dst = by_id + (size_t)b * tile_floats;
+// Gathered slabs (device after device, each in its ascending id order) -> tiles in bucket-id
+// order: slab tile i is bucket map[i].  One block per bucket.
+__global__ void k_unshard(const float* slabs, float* by_id, const uint32_t* map, uint32_t n_buckets, uint32_t tile_floats) {
+    const uint32_t i = blockIdx.x;
+    if (i >= n_buckets) return;
+    const float* src = slabs + (size_t)i * tile_floats;
+    float* dst = by_id + (size_t)map[i] * tile_floats;
     for (uint32_t k = threadIdx.x; k < tile_floats; k += blockDim.x) dst[k] = src[k];
 }
 
@@ -129,7 +152,7 @@ int render_multi(nart_ctx* ctx, const nart_render_params* p, nart_pixel* image, 
     const size_t tile_floats = (size_t)g.tile_size * g.tile_size * 5;
     std::vector<std::vector<uint32_t>> ids(n);
     for (uint32_t d = 0; d < n; ++d) {
-        ids[d] = shard_ids(nb, n, d);
+        ids[d] = shard_ids(g.n_buckets_x, nb, n, d);
         const size_t bytes = std::max<size_t>(1, ids[d].size()) * tile_floats * 4;
         if ((rc = ensure_dev(ctx, ctx->devs[d], ctx->sub_tiles[d], ctx->sub_cap[d], bytes, "device tiles"))) return rc;
     }
@@ -225,8 +248,13 @@ int render_multi(nart_ctx* ctx, const nart_render_params* p, nart_pixel* image, 
     }
 
     // 3. bucket-id order, raster-order combine on device 0, image to the host
-    hipLaunchKernelGGL(k_unshard, dim3(nb), dim3(256), 0, s0, slabs, static_cast<float*>(ctx->d_byid), nb, n,
-                       (uint32_t)tile_floats);
+    std::vector<uint32_t> map;
+    map.reserve(nb);
+    for (uint32_t d = 0; d < n; ++d) map.insert(map.end(), ids[d].begin(), ids[d].end());
+    if ((rc = ensure_dev(ctx, dev0, ctx->d_slab_map, ctx->cap_slab_map, (size_t)nb * 4, "slab map"))) return rc;
+    HIPCHK(hipMemcpyAsync(ctx->d_slab_map, map.data(), (size_t)nb * 4, hipMemcpyHostToDevice, s0));
+    hipLaunchKernelGGL(k_unshard, dim3(nb), dim3(256), 0, s0, slabs, static_cast<float*>(ctx->d_byid),
+                       static_cast<const uint32_t*>(ctx->d_slab_map), nb, (uint32_t)tile_floats);
     HIPCHK(hipGetLastError());
     if ((rc = nart_hip_combine_async(ctx->subs[0], p, static_cast<const nart_pixel*>(ctx->d_byid),
                                      static_cast<nart_pixel*>(ctx->d_image), s0)))

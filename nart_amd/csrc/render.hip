@@ -76,6 +76,10 @@ struct nart_ctx {
     uint32_t* d_keys[2] = {nullptr, nullptr};
     uint32_t* d_vals[2] = {nullptr, nullptr};
     uint32_t* d_qhead = nullptr;
+    uint32_t* d_cqueue = nullptr;  // split launch: the costliest pixels' dedicated waves
+    uint32_t cap_cqueue = 0;
+    hipStream_t st2 = nullptr;     // split launch: second stream of the device
+    hipEvent_t ev_split[2] = {nullptr, nullptr};
     void* d_sort_tmp = nullptr;
     size_t cap_sort_tmp = 0;
     uint32_t cap_queue = 0;
@@ -99,8 +103,8 @@ struct nart_ctx {
     bool bvh_on_device = false;
     double bvh_ms = 0.0;
     uint32_t num_leaf_tris = 0;
-    void *d_gather = nullptr, *d_byid = nullptr, *d_image = nullptr;
-    size_t cap_gather = 0, cap_byid = 0, cap_image = 0;
+    void *d_gather = nullptr, *d_byid = nullptr, *d_image = nullptr, *d_slab_map = nullptr;
+    size_t cap_gather = 0, cap_byid = 0, cap_image = 0, cap_slab_map = 0;
 };
 
 namespace {
@@ -509,6 +513,25 @@ __global__ void k_slot_rows(uint32_t n, uint32_t spp, SlotSO* so) {
     if (i < n) so[i] = SlotSO{(unsigned long long)i * spp, 1u, 0u};
 }
 
+// Sort keys of single pixels, costliest first (ascending sort of ~cost), values = slot ids.
+__global__ void k_cost_keys(const uint32_t* cost, uint32_t n, uint32_t* keys, uint32_t* vals) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    keys[i] = ~cost[i];
+    vals[i] = i;
+}
+
+// Split launch, the chains' queue: wave w holds chains w*per .. w*per+per-1 of the cost-sorted
+// list, chain c on the Q adjacent lanes (c % per)*Q .. +Q-1 (speculative lane group); every other
+// lane of the wave holds no pixel and only traces the wave's queued rays.
+__global__ void k_chain_queue(const uint32_t* sorted, uint32_t K, uint32_t per, uint32_t Q, uint32_t len,
+                              uint32_t* q) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= len) return;
+    const uint32_t w = p / 64u, j = p % 64u, c = w * per + j / Q;
+    q[p] = (j < per * Q && c < K) ? (sorted[c] | RQ_PRIO_BIT | (Q > 1u ? RQ_PAIR_BIT : 0u)) : 0xFFFFFFFFu;
+}
+
 __global__ void k_iota(uint32_t* v, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) v[i] = i;
@@ -518,12 +541,8 @@ __global__ void k_iota(uint32_t* v, uint32_t n) {
 #define NART_RQ_GROUP_LANES 2
 #endif
 int queue_mode() {
-    static int m = -1;
-    if (m < 0) {
-        const char* e = std::getenv("NART_QUEUE");
-        m = e ? std::max(0, std::min(2, std::atoi(e))) : 2;
-    }
-    return m;
+    const char* e = std::getenv("NART_QUEUE");
+    return e ? std::max(0, std::min(2, std::atoi(e))) : 2;
 }
 
 int sort_groups_by_cost(nart_ctx* ctx, uint32_t n, uint32_t* out, hipStream_t st) {
@@ -535,6 +554,22 @@ int sort_groups_by_cost(nart_ctx* ctx, uint32_t n, uint32_t* out, hipStream_t st
                                               ctx->d_vals[1], (int)ng, 0, 32, st));
     hipLaunchKernelGGL(k_expand_groups, dim3((n + 255) / 256), dim3(256), 0, st, ctx->d_vals[1], n, out);
     HIPCHK(hipGetLastError());
+    return NART_OK;
+}
+
+// Radix-sort scratch for a 32-bit-key sort of n pairs (grown on demand; the stream is drained first
+// because the scratch may be in use by work already queued on it).
+int ensure_sort_tmp(nart_ctx* ctx, uint32_t n, hipStream_t st) {
+    size_t need = 0;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, need, ctx->d_keys[0], ctx->d_keys[1], ctx->d_vals[0], ctx->d_vals[1],
+                                              (int)n, 0, 32));
+    if (need + 256 <= ctx->cap_sort_tmp) return NART_OK;
+    HIPCHK(hipStreamSynchronize(st));
+    if (ctx->d_sort_tmp) hipFree(ctx->d_sort_tmp);
+    ctx->d_sort_tmp = nullptr;
+    ctx->cap_sort_tmp = 0;
+    HIPCHK(hipMalloc(&ctx->d_sort_tmp, need + 256));
+    ctx->cap_sort_tmp = need + 256;
     return NART_OK;
 }
 
@@ -558,12 +593,12 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     // run k_render (256-lane blocks, stack_depth * 2 KiB) instead -- same image.
     const bool rq = ctx->variant == 0 && rq_fits(ctx);
     // camera rays first, coherently (k_primary); NART_PRIMARY=0 leaves them to the path kernel
-    static const bool primary = !std::getenv("NART_PRIMARY") || std::atoi(std::getenv("NART_PRIMARY")) != 0;
+    const bool primary = !std::getenv("NART_PRIMARY") || std::atoi(std::getenv("NART_PRIMARY")) != 0;
 
     // NART_QUORUM_MIN_ROUNDS: rounds of resident waves from which the quorum kernel is used (C3:
     // whole frame 16 rounds 569 -> 517 ms with it, 1/2 frame 8 rounds 332 -> 301, 1/4 4 rounds
     // 183 -> 179, 1/8 2 rounds 108 -> 134)
-    static const double q_rounds =
+    const double q_rounds =
         std::getenv("NART_QUORUM_MIN_ROUNDS") ? std::atof(std::getenv("NART_QUORUM_MIN_ROUNDS")) : 3.0;
     RenderArgs b = a;
     b.lds_nodes = render_lds_nodes(ctx);
@@ -599,7 +634,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             // traversal-phase quorum: 8 on throughput-bound launches; 0 (every queued ray resolved
             // before the path phase) on small shards, whose costliest pixels' chains set the time
             // (1/8 C3 shard: 100.5 -> 96.0 ms)
-            static const int rqq = std::getenv("NART_RQ_QUORUM") ? std::atoi(std::getenv("NART_RQ_QUORUM")) : -1;
+            const int rqq = std::getenv("NART_RQ_QUORUM") ? std::atoi(std::getenv("NART_RQ_QUORUM")) : -1;
             RenderArgs r2 = args;
             r2.lds_nodes = brq.lds_nodes;
             r2.prim = brq.prim;
@@ -624,7 +659,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             // rounds: 241 -> 235 ms; C4 batches, ~9 rounds: 1385 -> 1566 Msamples/s).  Below that a
             // wave of costly groups outlasts the rest (1/4 shard, 4 rounds: 146 -> 211 ms), and
             // the probe-ordered pixel queue with priority lanes stays
-            static const double g_rounds =
+            const double g_rounds =
                 std::getenv("NART_RQ_GROUP_MIN_ROUNDS") ? std::atof(std::getenv("NART_RQ_GROUP_MIN_ROUNDS")) : 6.0;
             if (R >= (rq ? g_rounds : 12.0) && mode == 2 && !std::getenv("NART_QUEUE_K")) {
                 // many rounds: the slot order (costly waves interleaved with cheap ones in time)
@@ -675,6 +710,80 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                 }
                 launch(blocks, b);
                 HIPCHK(hipGetLastError());
+                return NART_OK;
+            }
+            // split launch (NART_RQ_SPLIT=K, read per call): the K costliest single pixels of the cost
+            // probe run as dedicated waves on a second stream (per chains of Q speculative lanes in
+            // each, the other lanes only tracing their rays), so that their serial chains see
+            // little contention; the other pixels fill the device from a slot-order refill queue
+            const char* se = std::getenv("NART_RQ_SPLIT");
+            uint32_t K = se ? (uint32_t)std::max(0, std::atoi(se)) : 0u;
+            if (rq && mode == 2 && K > 0 && R < q_rounds) {
+                const char* qe = std::getenv("NART_RQ_SPLIT_Q");
+                const char* pe = std::getenv("NART_RQ_SPLIT_PER");
+                const char* ps = std::getenv("NART_RQ_SPLIT_PROBE");
+                const uint32_t Q = qe ? (std::atoi(qe) >= 4 ? 4u : (std::atoi(qe) >= 2 ? 2u : 1u)) : 4u;
+                const uint32_t per = std::max(1u, std::min(64u / Q, pe ? (uint32_t)std::atoi(pe) : 1u));
+                const uint32_t pspp = std::max(1u, std::min(a.spp, ps ? (uint32_t)std::atoi(ps) : 1u));
+                K = std::min(K, n / 2u);
+                const uint32_t Wc = (K + per - 1u) / per, clen = Wc * 64u;
+                RenderArgs pb = b;  // cost probe: the first pspp samples of every pixel
+                pb.spp = pspp;
+                pb.cost = ctx->d_cost;
+                hipLaunchKernelGGL((k_render<MAXL, true, ENV, false>), dim3(blocks), block, lds, st, ctx->scene, pb);
+                hipLaunchKernelGGL(k_cost_keys, eg, block, 0, st, ctx->d_cost, n, ctx->d_keys[0], ctx->d_vals[0]);
+                if (int rc3 = ensure_sort_tmp(ctx, n, st)) return rc3;
+                size_t tmp = ctx->cap_sort_tmp;
+                HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->d_sort_tmp, tmp, ctx->d_keys[0], ctx->d_keys[1],
+                                                          ctx->d_vals[0], ctx->d_vals[1], (int)n, 0, 32, st));
+                if (clen > ctx->cap_cqueue) {
+                    HIPCHK(hipStreamSynchronize(st));
+                    if (ctx->d_cqueue) hipFree(ctx->d_cqueue);
+                    ctx->d_cqueue = nullptr;
+                    ctx->cap_cqueue = 0;
+                    HIPCHK(hipMalloc(&ctx->d_cqueue, (size_t)clen * 4));
+                    ctx->cap_cqueue = clen;
+                }
+                hipLaunchKernelGGL(k_chain_queue, dim3((clen + 255) / 256), block, 0, st, ctx->d_vals[1], K, per, Q, clen,
+                                   ctx->d_cqueue);
+                // the other pixels in slot order: stable 1-bit partition by "is one of the K"
+                hipLaunchKernelGGL(k_flag_top, eg, block, 0, st, ctx->d_vals[1], n, K, ctx->d_keys[0]);
+                hipLaunchKernelGGL(k_iota, eg, block, 0, st, ctx->d_cost, n);
+                tmp = ctx->cap_sort_tmp;
+                HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->d_sort_tmp, tmp, ctx->d_keys[0], ctx->d_keys[1], ctx->d_cost,
+                                                          ctx->d_queue, (int)n, 0, 1, st));
+                if (!ctx->st2) {
+                    HIPCHK(hipStreamCreateWithFlags(&ctx->st2, hipStreamNonBlocking));
+                    for (auto& e : ctx->ev_split) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                }
+                HIPCHK(hipEventRecord(ctx->ev_split[0], st));
+                HIPCHK(hipStreamWaitEvent(ctx->st2, ctx->ev_split[0], 0));
+                RenderArgs c = b;
+                c.queue = ctx->d_cqueue;
+                c.qlen = clen;
+                c.qhead = nullptr;
+                c.rq_prio = 1u;
+                c.rq_pairs = Q > 1u ? Q : 0u;
+                c.rq_quorum = 0u;
+                c.lds_nodes = brq.lds_nodes;
+                c.prim = brq.prim;
+                hipLaunchKernelGGL(kern_rq, dim3((clen + NART_RQ_BLOCK - 1) / NART_RQ_BLOCK), dim3(NART_RQ_BLOCK), lds_rq,
+                                   ctx->st2, ctx->scene, c);
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipEventRecord(ctx->ev_split[1], ctx->st2));
+                RenderArgs bb = b;
+                bb.queue = ctx->d_queue;
+                bb.qlen = n - K;
+                bb.rq_prio = 0u;
+                bb.rq_pairs = 0u;
+                HIPCHK(hipMemsetAsync(ctx->d_qhead, 0, sizeof(uint32_t), st));
+                bb.qhead = ctx->d_qhead;
+                const uint32_t perb = NART_RQ_BLOCK / 256;
+                const uint32_t bblocks = (resident + perb - 1u) / perb * perb;
+                bb.qbase = bblocks * 256;
+                launch(bblocks, bb);
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipStreamWaitEvent(st, ctx->ev_split[1], 0));
                 return NART_OK;
             }
             if (const char* e = std::getenv("NART_QUEUE_K")) k = (uint32_t)std::max(1, std::min(64, std::atoi(e)));
@@ -758,10 +867,10 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     const dim3 block(256);
     const uint32_t blocks = (a.n_slots + 255) / 256;
     // NART_VOL_SM=0: the per-sample lock-step kernel (A/B timing only; same output)
-    static const bool sm = !(std::getenv("NART_VOL_SM") && std::getenv("NART_VOL_SM")[0] == '0');
+    const bool sm = !(std::getenv("NART_VOL_SM") && std::getenv("NART_VOL_SM")[0] == '0');
     RenderArgs b = a;
     // small density grids (C5: 2x2x2) are read from LDS (NART_VOL_LDS=0: from global memory)
-    static const bool vol_lds = !(std::getenv("NART_VOL_LDS") && std::getenv("NART_VOL_LDS")[0] == '0');
+    const bool vol_lds = !(std::getenv("NART_VOL_LDS") && std::getenv("NART_VOL_LDS")[0] == '0');
     const uint32_t nd = ctx->scene.medium.present ? ctx->scene.medium.rx * ctx->scene.medium.ry * ctx->scene.medium.rz : 0;
     b.lds_nodes = (sm && vol_lds && nd <= 4096u) ? nd : 0u;
     const size_t dl = (size_t)b.lds_nodes * sizeof(float);
@@ -773,27 +882,62 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_render_volume_sm<false, 1>, 256, dl));
     const uint32_t resident = (uint32_t)std::max(1, cus * std::max(per_cu, 1));
-    static const double w4_rounds = std::getenv("NART_VOL_W4_ROUNDS") ? std::atof(std::getenv("NART_VOL_W4_ROUNDS")) : 8.0;
+    const double w4_rounds = std::getenv("NART_VOL_W4_ROUNDS") ? std::atof(std::getenv("NART_VOL_W4_ROUNDS")) : 8.0;
     const bool w4 = (double)blocks / (double)resident >= w4_rounds;
+    uint32_t grid = blocks;
     if (queue_mode() == 2) {
         const uint32_t n = a.n_slots;
         if (blocks > resident && (double)n / (256.0 * resident) < 12.0 && a.spp > 4) {
-            int rc = ensure_queue(ctx, n);
+            const uint32_t W = resident * 4;  // resident waves
+            int rc = ensure_queue(ctx, n + 63u * W);
             if (rc) return rc;
             RenderArgs pb = b;
             pb.spp = 4;
             pb.cost = ctx->d_cost;
             if (sm) hipLaunchKernelGGL((k_render_volume_sm<false, 1>), dim3(blocks), block, dl, st, ctx->scene, pb);
             else hipLaunchKernelGGL((k_render_volume<false>), dim3(blocks), block, 0, st, ctx->scene, pb);
-            rc = sort_groups_by_cost(ctx, n, ctx->d_queue, st);
-            if (rc) return rc;
-            b.queue = ctx->d_queue;
+            // NART_VOL_K (read per call): costly pixels dealt to each wave of the first round, the
+            // waves persistent (a lane whose pixel is done takes the next queue entry).  A frame's
+            // costliest volume pixels cluster (C5: the image centre, 32 ms alone at 1,024 spp
+            // against 3 ms at the corners), so whole costly groups made waves of 64 long chains
+            // (one 8x8 wave of them: 66 ms alone).  0: the costliest wave-sized groups first.
+            const char* ke = std::getenv("NART_VOL_K");
+            const uint32_t k = std::min(64u, ke ? (uint32_t)std::max(0, std::atoi(ke)) : 2u);
+            if (k == 0 || !sm || (uint64_t)k * W > n) {
+                rc = sort_groups_by_cost(ctx, n, ctx->d_queue, st);
+                if (rc) return rc;
+                b.queue = ctx->d_queue;
+            } else {
+                const dim3 eg((n + 255) / 256);
+                hipLaunchKernelGGL(k_cost_keys, eg, block, 0, st, ctx->d_cost, n, ctx->d_keys[0], ctx->d_vals[0]);
+                if ((rc = ensure_sort_tmp(ctx, n, st))) return rc;
+                size_t tmp = ctx->cap_sort_tmp;
+                HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->d_sort_tmp, tmp, ctx->d_keys[0], ctx->d_keys[1],
+                                                          ctx->d_vals[0], ctx->d_vals[1], (int)n, 0, 32, st));
+                hipLaunchKernelGGL(k_flag_top, eg, block, 0, st, ctx->d_vals[1], n, k * W, ctx->d_keys[0]);
+                hipLaunchKernelGGL(k_iota, eg, block, 0, st, ctx->d_cost, n);
+                tmp = ctx->cap_sort_tmp;
+                HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->d_sort_tmp, tmp, ctx->d_keys[0], ctx->d_keys[1], ctx->d_cost,
+                                                          ctx->d_vals[0], (int)n, 0, 1, st));
+                hipLaunchKernelGGL(k_build_queue, eg, block, 0, st, ctx->d_vals[1], ctx->d_vals[0], n, W, k, 0u, 0u,
+                                   ctx->d_queue);
+                HIPCHK(hipMemsetAsync(ctx->d_qhead, 0, sizeof(uint32_t), st));
+                b.queue = ctx->d_queue;
+                b.qhead = ctx->d_qhead;
+                b.qlen = n;
+                int pc = 0;
+                HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                    &pc, w4 ? (const void*)k_render_volume_sm<false, 4> : (const void*)k_render_volume_sm<false, 1>, 256, dl));
+                grid = (uint32_t)std::max(1, cus * std::max(pc, 1));
+                b.qbase = grid * 256;
+            }
+            HIPCHK(hipGetLastError());
         }
     }
     if (sm) {
-        if (ctx->counters) hipLaunchKernelGGL((k_render_volume_sm<true, 1>), dim3(blocks), block, dl, st, ctx->scene, b);
-        else if (w4) hipLaunchKernelGGL((k_render_volume_sm<false, 4>), dim3(blocks), block, dl, st, ctx->scene, b);
-        else hipLaunchKernelGGL((k_render_volume_sm<false, 1>), dim3(blocks), block, dl, st, ctx->scene, b);
+        if (ctx->counters) hipLaunchKernelGGL((k_render_volume_sm<true, 1>), dim3(grid), block, dl, st, ctx->scene, b);
+        else if (w4) hipLaunchKernelGGL((k_render_volume_sm<false, 4>), dim3(grid), block, dl, st, ctx->scene, b);
+        else hipLaunchKernelGGL((k_render_volume_sm<false, 1>), dim3(grid), block, dl, st, ctx->scene, b);
     } else {
         if (ctx->counters) hipLaunchKernelGGL((k_render_volume<true>), dim3(blocks), block, 0, st, ctx->scene, b);
         else hipLaunchKernelGGL((k_render_volume<false>), dim3(blocks), block, 0, st, ctx->scene, b);
@@ -891,7 +1035,7 @@ bool splat_lut(const float thr[65], const float table[64], std::vector<float4>& 
 // slot once there are >= 64 slots), the global-memory variant beyond.
 int launch_latin(nart_ctx* ctx, const RenderArgs& ra, hipStream_t st) {
     // three-kernel form (k_latin_draws / _perm / _emit) when its scratch fits in Lout
-    static const int latin_env = std::getenv("NART_LATIN") ? std::atoi(std::getenv("NART_LATIN")) : -1;
+    const int latin_env = std::getenv("NART_LATIN") ? std::atoi(std::getenv("NART_LATIN")) : -1;
     const uint32_t groups = (ra.n_slots + 63) / 64;
     LatinScratch ls;
     ls.n2 = (ra.spp + 1) / 2;
@@ -949,7 +1093,7 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
     HIPCHK(hipMemcpy(ctx->d_table, table, sizeof(table), hipMemcpyHostToDevice));
     std::vector<float4> lut;
     uint32_t lut_b0 = 0;
-    static const bool lut_env = !(std::getenv("NART_SPLAT_LUT") && std::getenv("NART_SPLAT_LUT")[0] == '0');
+    const bool lut_env = !(std::getenv("NART_SPLAT_LUT") && std::getenv("NART_SPLAT_LUT")[0] == '0');
     const bool lut_ok = lut_env && thr_ok && splat_lut(table + 64, table, lut, lut_b0);
     // skewed-time splat (k_splat_skew, pixel-major samples) where its preconditions hold, else
     // k_splat_col4 / k_splat over the sample-major layout
@@ -957,7 +1101,7 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
     // launch has fewer than ~2 waves per SIMD: small shards keep k_splat_col4 (C5 1/8 shard:
     // 54 ms skewed vs 23 ms col4; whole frame 72 vs 113 ms).  NART_SKEW_MIN_WAVES: waves per SIMD.
     const uint32_t B = p->bucket_size, tile = B + 2 * g.filter_bounds;
-    static const double skew_min =
+    const double skew_min =
         std::getenv("NART_SKEW_MIN_WAVES") ? std::atof(std::getenv("NART_SKEW_MIN_WAVES")) : 2.0;
     int n_cus = 0;
     HIPCHK(hipDeviceGetAttribute(&n_cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
@@ -1556,7 +1700,7 @@ void nart_hip_destroy(nart_ctx* ctx) {
             if (d < ctx->streams.size() && ctx->streams[d]) hipStreamDestroy(ctx->streams[d]);
         }
         hipSetDevice(ctx->devs[0]);
-        for (void* b : {ctx->d_gather, ctx->d_byid, ctx->d_image})
+        for (void* b : {ctx->d_gather, ctx->d_byid, ctx->d_image, ctx->d_slab_map})
             if (b) hipFree(b);
         for (nart_ctx* c : ctx->subs) nart_hip_destroy(c);
         delete ctx;
@@ -1568,9 +1712,13 @@ void nart_hip_destroy(nart_ctx* ctx) {
                     ctx->d_L, ctx->d_bucket_ids, ctx->d_bucket_base, ctx->d_table, ctx->d_lut, ctx->d_counters, ctx->d_envs, ctx->d_density,
                     ctx->d_oc_nodes, ctx->d_oc_chunks, ctx->d_oc_tris, ctx->d_tri_leaf, ctx->d_oc_lock, ctx->d_oc_heap,
                     ctx->d_queue, ctx->d_cost, ctx->d_keys[0], ctx->d_keys[1], ctx->d_vals[0], ctx->d_vals[1],
-                    ctx->d_qhead, ctx->d_sort_tmp};
+                    ctx->d_qhead, ctx->d_sort_tmp, ctx->d_cqueue};
     for (void* b : bufs)
         if (b) hipFree(b);
+    if (ctx->st2) {
+        hipStreamDestroy(ctx->st2);
+        for (auto& e : ctx->ev_split) hipEventDestroy(e);
+    }
     for (void* b : ctx->env_bufs) hipFree(b);
     if (ctx->events)
         for (auto& e : ctx->ev) hipEventDestroy(e);
@@ -1851,10 +1999,10 @@ int nart_hip_device_count(int* count) {
     return NART_OK;
 }
 
-int nart_hip_shard_buckets(uint32_t n_buckets, uint32_t n_devices, uint32_t device_index, uint32_t* ids,
-                           uint32_t* count) {
-    if (!count || !n_devices || device_index >= n_devices) return NART_E_INVALID;
-    const std::vector<uint32_t> v = shard_ids(n_buckets, n_devices, device_index);
+int nart_hip_shard_buckets(uint32_t n_buckets_x, uint32_t n_buckets, uint32_t n_devices, uint32_t device_index,
+                           uint32_t* ids, uint32_t* count) {
+    if (!count || !n_devices || !n_buckets_x || device_index >= n_devices) return NART_E_INVALID;
+    const std::vector<uint32_t> v = shard_ids(n_buckets_x, n_buckets, n_devices, device_index);
     if (ids) std::memcpy(ids, v.data(), v.size() * sizeof(uint32_t));
     *count = (uint32_t)v.size();
     return NART_OK;

@@ -2,8 +2,8 @@
 
 The reference renders the 16x16 buckets of a session with a tbb::task_group and sums their
 tiles into the image in bucket raster order (render.cpp:152-203).  Across ranks:
-  * rank r renders buckets r, r + N, r + 2N, ... (interleaved: the costly sphere region spreads
-    evenly over ranks, with no host work queue);
+  * rank r renders the buckets bucket_owners assigns it (diagonal-lattice interleave: the
+    costly sphere region spreads evenly over ranks, with no host work queue);
   * each rank's tiles (tileSize^2 Pixels per bucket) are gathered to rank 0 with one
     torch.distributed gather (RCCL over xGMI on GPUs; gloo in the CPU tests, and in the
     one-GPU multi-rank test, where device tiles are staged through host memory);
@@ -15,6 +15,7 @@ spawn_ranks starts the one-process-per-GPU job itself when a script is run with 
 launcher (torch.distributed.run) set up the rendezvous: N children with RANK / LOCAL_RANK /
 WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT, started before the parent touches any GPU.
 """
+import math
 import os
 import socket
 import subprocess
@@ -62,19 +63,41 @@ def spawn_ranks(n, argv, env=None):
     return rc
 
 
+def lattice_step(world):
+    """Row shift s of the diagonal lattice: the s in [1, world) coprime to world closest to 0.382
+    world (golden section: neighbouring rows' owners are far apart), 0 for one rank."""
+    cands = [s for s in range(1, world) if math.gcd(s, world) == 1]
+    return min(cands, key=lambda s: abs(s - 0.382 * world)) if cands else 0
+
+
+def bucket_owners(n_buckets_x, n_buckets, world, scheme="lattice"):
+    """Owner rank of every bucket id (by * n_buckets_x + bx).  "lattice" (default): a diagonal
+    lattice, owner = (bx + s * by) % world with s = lattice_step(world): every run of `world`
+    buckets along a row or column holds each rank once, so every region of the frame -- the costly
+    glass of C3 -- splits evenly over the ranks.  "mod": b % world, which with a bucket-column count
+    divisible by world gives each rank whole vertical stripes (C3 1/8 shards 86-101 ms).  Must
+    match shard_ids in host/multi_gpu.h (nart_hip_shard_buckets)."""
+    b = np.arange(n_buckets, dtype=np.int64)
+    if scheme == "mod" or world == 1:
+        return b % world
+    return (b % n_buckets_x + lattice_step(world) * (b // n_buckets_x)) % world
+
+
 class BucketShard:
     """Bucket ownership and the tile gather for one rank of an N-rank render."""
 
-    def __init__(self, n_buckets, tile_pixels, rank, world, device):
+    def __init__(self, n_buckets_x, n_buckets, tile_pixels, rank, world, device, scheme=None):
         self.nb, self.tpx, self.rank, self.world = n_buckets, tile_pixels, rank, world
-        self.mine = np.arange(rank, n_buckets, world, dtype=np.uint32)
-        self.per_rank = (n_buckets + world - 1) // world
+        scheme = scheme or os.environ.get("NART_SHARD", "lattice")
+        owners = bucket_owners(n_buckets_x, n_buckets, world, scheme)
+        self.mine = np.nonzero(owners == rank)[0].astype(np.uint32)
+        self.per_rank = int(max(np.bincount(owners, minlength=world).max(), 1))
         self.tiles = torch.zeros((self.per_rank, tile_pixels, 5), dtype=torch.float32, device=device)
         self.gathered = self.by_id = None
         if rank == 0:
             self.gathered = torch.zeros((world, self.per_rank, tile_pixels, 5), dtype=torch.float32, device=device)
             self.by_id = torch.zeros((n_buckets, tile_pixels, 5), dtype=torch.float32, device=device)
-            owned = [np.arange(r, n_buckets, world) for r in range(world)]
+            owned = [np.nonzero(owners == r)[0] for r in range(world)]
             self.order = torch.from_numpy(np.concatenate(owned).astype(np.int64)).to(device)
             self.slots = torch.from_numpy(np.concatenate(
                 [r * self.per_rank + np.arange(len(o)) for r, o in enumerate(owned)]).astype(np.int64)).to(device)

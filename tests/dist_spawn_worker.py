@@ -30,7 +30,7 @@ def main():
         p.image_width, p.image_height, p.spp = w, h, spp
         g = nart_amd.session_geometry(p)
         nb = g.n_buckets_x * g.n_buckets_y
-        shard = BucketShard(nb, g.tile_size * g.tile_size, rank, world, torch.device("cpu"))
+        shard = BucketShard(g.n_buckets_x, nb, g.tile_size * g.tile_size, rank, world, torch.device("cpu"))
         t = oracle.Oracle(scene).render_buckets(p, shard.mine, 2)
         shard.tiles[:len(shard.mine)] = torch.from_numpy(t)
         by_id = shard.gather()

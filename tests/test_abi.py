@@ -90,14 +90,33 @@ def test_bvh_depth_cap(built, glass_scene, monkeypatch):
 
 def test_multi_device_shard_partition(built):
     """nart_hip_shard_buckets (host only): the multi-device context's buckets per device partition
-    the frame (every bucket exactly once, ascending per device, b % n == device)."""
+    the frame (every bucket exactly once, ascending per device), and the C ABI deals exactly as the
+    one-process-per-GPU path does (nart_amd.dist.bucket_owners)."""
     import numpy as np
-    for nb_, n in [(8160, 8), (15, 2), (7, 4), (3, 8), (32400, 8), (1, 1)]:
-        parts = [nart_amd.shard_buckets(nb_, n, d) for d in range(n)]
+    from nart_amd.dist import bucket_owners
+    for nbx, nb_, n in [(120, 8160, 8), (5, 15, 2), (7, 7, 4), (3, 3, 8), (240, 32400, 8), (1, 1, 1), (13, 104, 6)]:
+        parts = [nart_amd.shard_buckets(nbx, nb_, n, d) for d in range(n)]
         allb = np.concatenate(parts)
         assert np.array_equal(np.sort(allb), np.arange(nb_))
+        owners = bucket_owners(nbx, nb_, n)
         for d, ids in enumerate(parts):
-            assert np.all(ids % n == d) and np.all(np.diff(ids.astype(np.int64)) > 0)
+            assert np.array_equal(ids, np.nonzero(owners == d)[0]) and np.all(np.diff(ids.astype(np.int64)) > 0)
+
+
+def test_shard_spreads_regions_evenly():
+    """Every block of the bucket grid (e.g. the C3 glass region) splits over 8 devices within a
+    bucket or two per device, unlike b % 8 (whole stripes: a 4-bucket-wide column on 4 devices)."""
+    import numpy as np
+    from nart_amd.dist import bucket_owners
+    nbx, nby = 120, 68
+    b = np.arange(nbx * nby)
+    lat, mod = bucket_owners(nbx, nbx * nby, 8), bucket_owners(nbx, nbx * nby, 8, "mod")
+    for x0, x1, y0, y1 in [(40, 80, 20, 60), (50, 70, 30, 50), (58, 62, 40, 50), (0, 120, 0, 68)]:
+        region = (b % nbx >= x0) & (b % nbx < x1) & (b // nbx >= y0) & (b // nbx < y1)
+        per = np.bincount(lat[region], minlength=8)
+        assert per.max() - per.min() <= 2, per
+    region = (b % nbx >= 58) & (b % nbx < 62)
+    assert np.bincount(mod[region], minlength=8).min() == 0
 
 
 def test_multi_device_create_without_gpu_fails_cleanly(built, glass_scene):

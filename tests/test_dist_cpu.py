@@ -34,7 +34,7 @@ def _worker(rank, world, port, scene_path, w, h, spp, out_path):
         p.image_width, p.image_height, p.spp = w, h, spp
         g = nart_amd.session_geometry(p)
         nb = g.n_buckets_x * g.n_buckets_y
-        shard = BucketShard(nb, g.tile_size * g.tile_size, rank, world, torch.device("cpu"))
+        shard = BucketShard(g.n_buckets_x, nb, g.tile_size * g.tile_size, rank, world, torch.device("cpu"))
         t = oracle.Oracle(scene).render_buckets(p, shard.mine, 2)
         shard.tiles[:len(shard.mine)] = torch.from_numpy(t)
         by_id = shard.gather()
@@ -62,6 +62,9 @@ def test_sharded_gather_matches_single_process(built, glass_scene, tmp_path, wor
 def test_bucket_ownership_partitions():
     from nart_amd.dist import BucketShard
     import torch
-    for nb, world in [(8160, 8), (15, 2), (7, 4), (3, 8)]:
-        owned = np.concatenate([BucketShard(nb, 4, r, world, torch.device("cpu")).mine for r in range(world)])
+    for nbx, nb, world in [(120, 8160, 8), (5, 15, 2), (7, 7, 4), (3, 3, 8), (13, 104, 3)]:
+        parts = [BucketShard(nbx, nb, 4, r, world, torch.device("cpu")).mine for r in range(world)]
+        owned = np.concatenate(parts)
         assert np.array_equal(np.sort(owned), np.arange(nb))
+        sizes = [len(x) for x in parts]
+        assert max(sizes) - min(sizes) <= (nb // nbx + 1), sizes

@@ -41,7 +41,7 @@ def _worker(rank, world, port, scene_path, w, h, spp, out_path):
         nb = g.n_buckets_x * g.n_buckets_y
         gpu = nart_amd.HipRenderer(scene, device=0)
         stream = torch.cuda.current_stream()
-        shard = BucketShard(nb, g.tile_size * g.tile_size, rank, world, dev)
+        shard = BucketShard(g.n_buckets_x, nb, g.tile_size * g.tile_size, rank, world, dev)
         gpu.render_buckets_async(p, shard.mine, shard.tiles.data_ptr(), stream.cuda_stream)
         torch.cuda.synchronize()
         by_id = shard.gather()

@@ -120,6 +120,22 @@ def test_queue_speculative_pairs(gpu, glass_scene, monkeypatch, pairs):
     assert _bits_equal(g, r), _report(g, r)
 
 
+@pytest.mark.parametrize("k,q,per", [("300", "4", "1"), ("300", "2", "2"), ("200", "1", "4")],
+                         ids=["quads-1", "pairs-2", "single-4"])
+def test_split_launch_chains(gpu, glass_scene, monkeypatch, k, q, per):
+    """Split launch of a small shard: the k costliest pixels of the cost probe as dedicated waves
+    (per chains of q speculative lanes each) on a second stream, the rest from a slot-order
+    refill queue on the caller's stream.  Only where and when each pixel's chain runs changes;
+    the frame must equal the oracle's bit for bit."""
+    monkeypatch.setenv("NART_RQ_SPLIT", k)
+    monkeypatch.setenv("NART_RQ_SPLIT_Q", q)
+    monkeypatch.setenv("NART_RQ_SPLIT_PER", per)
+    p = _params(glass_scene, 512, 300, 24)
+    g = nart_amd.HipRenderer(glass_scene, variant=0).render(p)
+    r = oracle.Oracle(glass_scene).render(p)
+    assert _bits_equal(g, r), _report(g, r)
+
+
 @pytest.fixture(scope="module")
 def full_frame_1spp(glass_scene):
     """The C3 frame size at 1 spp: ~16 rounds of resident waves, so the ray-queue kernel runs its
@@ -212,10 +228,15 @@ def test_volume_integrator(gpu, volume_scenes, kind):
     assert _bits_equal(g, r), _report(g, r)
 
 
-def test_volume_queue_scheduler(gpu, volume_scenes):
+@pytest.mark.parametrize("k", ["2", "8", "0"], ids=["dealt-2", "dealt-8", "groups"])
+@pytest.mark.parametrize("kind", ["c5", "emissive"])
+def test_volume_queue_scheduler(gpu, volume_scenes, monkeypatch, kind, k):
     """More pixels than resident lanes: the volume kernel runs its cost probe (4 samples per
-    pixel) and launches the costliest pixel groups first (render.hip dispatch_volume)."""
-    sc = volume_scenes["c5"]
+    pixel); the costliest single pixels are dealt k per wave over the first round of persistent
+    waves whose lanes refill from the queue (NART_VOL_K=0: the costliest pixel groups first, one
+    lane per pixel; render.hip dispatch_volume).  Only the order of work changes."""
+    monkeypatch.setenv("NART_VOL_K", k)
+    sc = volume_scenes[kind]
     p = _params(sc, 640, 360, 8)
     g = nart_amd.HipRenderer(sc).render(p)
     r = oracle.Oracle(sc).render(p)

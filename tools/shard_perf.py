@@ -47,7 +47,7 @@ def main():
         ranks = range(n) if a.rank < 0 else [a.rank]
         per = []
         for r in ranks:
-            shard = BucketShard(nb, tpx, r, n, dev)
+            shard = BucketShard(g.n_buckets_x, nb, tpx, r, n, dev)
             best = None
             for _ in range(a.reps):
                 st = nart_amd.RenderStats()
@@ -63,7 +63,7 @@ def main():
             per.append(best)
         worst = max(per, key=lambda d: d["wall_ms"])
         walls = [d["wall_ms"] for d in per]
-        print(json.dumps({"n": n, "buckets_per_rank": len(BucketShard(nb, tpx, 0, n, "cpu").mine),
+        print(json.dumps({"n": n, "buckets_per_rank": len(BucketShard(g.n_buckets_x, nb, tpx, 0, n, "cpu").mine),
                           "worst": {k: round(v, 3) for k, v in worst.items()},
                           "spread": {"min_ms": round(min(walls), 3), "max_ms": round(max(walls), 3),
                                      "mean_ms": round(sum(walls) / len(walls), 3)},
