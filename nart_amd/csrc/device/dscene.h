@@ -88,6 +88,16 @@ struct DMedium {
     float Le[3];
     float maj[8];
     const float* density;
+    // exact strength reductions (host-checked, build_medium): x / d == x * (1/d) bit for bit when d
+    // is a power of two whose reciprocal is a normal float (both are the correctly rounded x * 2^-k)
+    float inv_bs[3];       // 1 / (bmax - bmin) per axis, valid where bit i of bs_pow2 is set
+    uint32_t bs_pow2;
+    float inv_maj[8];      // 1 / maj[j], valid where bit j of maj_pow2 is set
+    uint32_t maj_pow2;
+    // 2x2x2 grids: the 8 densities in the kernel arguments (DensityGrid::LookUp then always reads
+    // corners 0/1 of each axis: no memory access, same arithmetic)
+    uint32_t grid2;
+    float dens8[8];
 };
 
 // Reference octree (bvh.cpp:115-250), kept beside the device BVH so that the render path can

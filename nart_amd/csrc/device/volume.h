@@ -42,6 +42,23 @@ NHD float dg_lookup(const DMedium& m, const float* dens, f3 p) {  // media.cpp:1
     return gmix(y0, y1, zD);
 }
 
+// DensityGrid::LookUp on a 2x2x2 grid (m.grid2): every lookup reads corners lo = 0, hi = 1 of
+// each axis (x = clamp(p, 0, 0.999) * (2 - 1) truncates to 0), so the densities come from the
+// kernel arguments; the arithmetic is dg_lookup's, operation for operation.
+NHD float dg_lookup2(const DMedium& m, f3 p) {
+    const float xD = gmin(gmax(0.f, p.x), 0.999f) * 1.f - 0.f;
+    const float yD = gmin(gmax(0.f, p.y), 0.999f) * 1.f - 0.f;
+    const float zD = gmin(gmax(0.f, p.z), 0.999f) * 1.f - 0.f;
+    const float* d = m.dens8;  // index 4z + 2y + x (dg_at with rx = ry = 2)
+    const float x0 = gmix(d[0], d[1], xD);
+    const float x1 = gmix(d[4], d[5], xD);
+    const float x2 = gmix(d[2], d[3], xD);
+    const float x3 = gmix(d[6], d[7], xD);
+    const float y0 = gmix(x0, x2, yD);
+    const float y1 = gmix(x1, x3, yD);
+    return gmix(y0, y1, zD);
+}
+
 struct MajIter {  // RayMajorantIterator (media.cpp:138-255) for a width-1 grid
     float tCurrent, tMax;
     uint32_t idx;
@@ -73,12 +90,14 @@ ND bool medium_sample_ray(const DMedium& m, f3 o, f3 d, MajIter& it) {
     f3 pX = add(o, muls(d, tMax));
     const f3 bs = sub(bmax, bmin);
     pE = sub(pE, bmin);
-    pE = F3(pE.x / bs.x, pE.y / bs.y, pE.z / bs.z);
+    pE = m.bs_pow2 == 7u ? F3(pE.x * m.inv_bs[0], pE.y * m.inv_bs[1], pE.z * m.inv_bs[2])
+                         : F3(pE.x / bs.x, pE.y / bs.y, pE.z / bs.z);
     pE = F3(gmax(gmin(pE.x, 0.999999f), 0.f), gmax(gmin(pE.y, 0.999999f), 0.f), gmax(gmin(pE.z, 0.999999f), 0.f));
     pE = muls(pE, 1.f);
     it.idx = 0;
     pX = sub(pX, bmin);
-    pX = F3(pX.x / bs.x, pX.y / bs.y, pX.z / bs.z);
+    pX = m.bs_pow2 == 7u ? F3(pX.x * m.inv_bs[0], pX.y * m.inv_bs[1], pX.z * m.inv_bs[2])
+                         : F3(pX.x / bs.x, pX.y / bs.y, pX.z / bs.z);
     pX = F3(gmax(gmin(pX.x, 0.999999f), 0.f), gmax(gmin(pX.y, 0.999999f), 0.f), gmax(gmin(pX.z, 0.999999f), 0.f));
     pX = muls(pX, 1.f);
     f3 gD = normalize(sub(pX, pE));
@@ -101,7 +120,7 @@ ND bool medium_sample_ray(const DMedium& m, f3 o, f3 d, MajIter& it) {
     return true;
 }
 
-ND bool maj_next(const DMedium& m, MajIter& it, float& sigma, float& t0, float& t1) {  // media.cpp:214-255
+ND bool maj_next(const DMedium& m, MajIter& it, float& sigma, float& t0, float& t1, uint32_t* used = nullptr) {  // media.cpp:214-255
     if (it.tCurrent + 0.0001f > it.tMax) return false;
     uint32_t choice = 0;
     if (it.next.x < it.next.y) choice += 4;
@@ -116,6 +135,7 @@ ND bool maj_next(const DMedium& m, MajIter& it, float& sigma, float& t0, float& 
 #pragma unroll
     for (int j = 1; j < 8; ++j) sm = (int)it.idx == j ? m.maj[j] : sm;
     sigma = sm;
+    if (used) *used = it.idx;
     t0 = it.tCurrent;
     t1 = it.tCurrent + dt;
     const float nx = it.next.x - dt, ny = it.next.y - dt, nz = it.next.z - dt;
@@ -286,14 +306,27 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
     take(slot);
     const DMedium& m = S.medium;
     const f3 beta = F3(1.f, 1.f, 1.f);
-    enum { P_SAMPLE, P_RAY, P_MAJ, P_COLL, P_ESC };
+    enum { P_SAMPLE, P_RAY, P_MAJ, P_COLL, P_ESC, P_SCAT };
     uint32_t work = 0, s = 0, bounce = 0;
     int ph = P_SAMPLE;
     f3 o = F3(0.f, 0.f, 0.f), d = o, ro = o, rd = o, L = o;
     float uMode = 0.f, sigma = 1.f, tMin = 0.f, t1 = 0.f;
+    uint32_t sidx = 0;  // majorant entry of the current segment (sigma = m.maj[sidx])
     MajIter it;
     for (;;) {
         bool finish = false;
+        // Phase batching (A.vol_batch = F): the wave executes the union of its lanes' phases, and
+        // the rare ones -- a scatter direction (acosf + 2 sinf/cosf), a new ray segment through the
+        // medium box, the escape to the lights -- cost several times a tentative collision.  They
+        // run only when at least 1/F of the wave's active lanes wait for one (or no lane has a
+        // cheap phase left); until then those lanes idle while the others keep sampling
+        // collisions.  Each lane's own operations and their order are unchanged.
+        bool xok = true;
+        if (A.vol_batch) {
+            const bool cheap = ph == P_SAMPLE || ph == P_MAJ || ph == P_COLL;
+            const uint64_t mc = __ballot(cheap), me = __ballot(!cheap);
+            xok = mc == 0 || (uint32_t)__popcll(me) * A.vol_batch >= (uint32_t)__popcll(mc | me);
+        }
         if (ph == P_SAMPLE) {
             if (s >= A.spp) {
                 if (!A.qhead || A.cost) break;
@@ -310,7 +343,13 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
             bounce = 0;
             ph = P_RAY;
         }
-        if (ph == P_RAY) {  // top of VolumeIntegrator's bounce loop
+        if (ph == P_SCAT && xok) {  // isotropic scattering direction (volumeintegrator.cpp:44-47)
+            const float a = rng_float(rng);
+            const float b = rng_float(rng);
+            d = uniform_sample_sphere(F2(a, b));
+            ph = P_RAY;
+        }
+        if (ph == P_RAY && xok) {  // top of VolumeIntegrator's bounce loop
             (void)rng_float(rng);  // u: passed to SampleT_maj, unused there
             uMode = rng_float(rng);
             if (m.present && medium_sample_ray(m, o, d, it)) {
@@ -323,7 +362,7 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
         }
         if (ph == P_MAJ) {
             float t0;
-            if (maj_next(m, it, sigma, t0, t1)) {
+            if (maj_next(m, it, sigma, t0, t1, &sidx)) {
                 tMin = t0;
                 ph = P_COLL;
             } else {
@@ -332,11 +371,19 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
         }
         if (ph == P_COLL) {
             ++work;
-            const float t = tMin + (-glibc_logf_with(1.f - rng_float(rng), [&](int i, double& invc, double& logc) {
-                                         const double2 e = s_logf[i];
-                                         invc = e.x;
-                                         logc = e.y;
-                                     }) / sigma);
+            // sigma a power of two for every lane of the wave: multiply by its exact reciprocal
+            const bool sp2 = __ballot(!((m.maj_pow2 >> sidx) & 1u)) == 0;
+            float isig = m.inv_maj[0];
+#pragma unroll
+            for (int j = 1; j < 8; ++j) isig = (int)sidx == j ? m.inv_maj[j] : isig;
+            const float lg = -glibc_logf_with(1.f - rng_float(rng), [&](int i, double& invc, double& logc) {
+                const double2 e = s_logf[i];
+                invc = e.x;
+                logc = e.y;
+            });
+            float t;
+            if (sp2) t = tMin + lg * isig;
+            else t = tMin + lg / sigma;
             if (!(t < t1)) {
                 ph = P_MAJ;
             } else {
@@ -348,10 +395,18 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
                     const f3 bmin = F3(m.bmin[0], m.bmin[1], m.bmin[2]);
                     const f3 bs = sub(F3(m.bmax[0], m.bmax[1], m.bmax[2]), bmin);
                     const f3 q0 = sub(p, bmin);
-                    const float density = dg_lookup(m, dens, F3(q0.x / bs.x, q0.y / bs.y, q0.z / bs.z));
+                    const f3 qn = m.bs_pow2 == 7u ? F3(q0.x * m.inv_bs[0], q0.y * m.inv_bs[1], q0.z * m.inv_bs[2])
+                                                  : F3(q0.x / bs.x, q0.y / bs.y, q0.z / bs.z);
+                    const float density = m.grid2 ? dg_lookup2(m, qn) : dg_lookup(m, dens, qn);
                     const float sa = m.sigma_a * density, ss = m.sigma_s * density;
-                    const float pAbsorb = sa / sigma;
-                    const float pScatter = ss / sigma;
+                    float pAbsorb, pScatter;
+                    if (sp2) {
+                        pAbsorb = sa * isig;
+                        pScatter = ss * isig;
+                    } else {
+                        pAbsorb = sa / sigma;
+                        pScatter = ss / sigma;
+                    }
                     if (uMode < pAbsorb) {
                         L = add(L, mul(muls(F3(m.Le[0], m.Le[1], m.Le[2]), density), beta));
                         finish = true;
@@ -359,11 +414,8 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
                         if (bounce++ > A.bounces) {
                             finish = true;
                         } else {
-                            const float a = rng_float(rng);
-                            const float b = rng_float(rng);
                             o = p;
-                            d = uniform_sample_sphere(F2(a, b));
-                            ph = P_RAY;
+                            ph = P_SCAT;
                         }
                     } else {
                         uMode = rng_float(rng);  // null collision
@@ -372,7 +424,7 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
                 }
             }
         }
-        if (ph == P_ESC) {
+        if (ph == P_ESC && xok) {
             float lightTMax = __builtin_inff();
             f3 Le = F3(0.f, 0.f, 0.f);
             for (uint32_t j = 0; j < S.num_lights; ++j) {

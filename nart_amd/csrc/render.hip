@@ -273,6 +273,21 @@ int build_medium(nart_ctx* ctx, const nart_medium& bm, DMedium& m) {
         m.maj[2 + i] = bm.bounds_min[i];
         m.maj[5 + i] = bm.bounds_max[i];
     }
+    // exact reciprocals of power-of-two divisors (x / 2^k and x * 2^-k round the same real value)
+    auto pow2 = [](float x, float& inv) {
+        int e = 0;
+        if (!(x > 0.f) || !std::isfinite(x) || std::frexp(x, &e) != 0.5f) return false;
+        inv = 1.f / x;
+        return std::isnormal(inv) && std::frexp(inv, &e) == 0.5f;
+    };
+    for (int i = 0; i < 3; ++i)
+        if (pow2(m.bmax[i] - m.bmin[i], m.inv_bs[i])) m.bs_pow2 |= 1u << i;
+    for (int j = 0; j < 8; ++j)
+        if (pow2(m.maj[j], m.inv_maj[j])) m.maj_pow2 |= 1u << j;
+    if (m.rx == 2 && m.ry == 2 && m.rz == 2) {
+        m.grid2 = 1;
+        for (int i = 0; i < 8; ++i) m.dens8[i] = bm.density[i];
+    }
     int rc = upload(ctx, ctx->d_density, bm.density, npts);
     m.density = (const float*)ctx->d_density;
     return rc;
@@ -521,6 +536,14 @@ __global__ void k_cost_keys(const uint32_t* cost, uint32_t n, uint32_t* keys, ui
     vals[i] = i;
 }
 
+// Split launch, classes of the cost-sorted pixels: 2 the K dedicated chains, 1 the next E (the
+// priority pixels of the bulk launch), 0 the rest.
+__global__ void k_flag_classes(const uint32_t* sorted, uint32_t n, uint32_t K, uint32_t E, uint32_t* flag) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    flag[sorted[r]] = r < K ? 2u : (r < K + E ? 1u : 0u);
+}
+
 // Split launch, the chains' queue: wave w holds chains w*per .. w*per+per-1 of the cost-sorted
 // list, chain c on the Q adjacent lanes (c % per)*Q .. +Q-1 (speculative lane group); every other
 // lane of the wave holds no pixel and only traces the wave's queued rays.
@@ -746,12 +769,28 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                 }
                 hipLaunchKernelGGL(k_chain_queue, dim3((clen + 255) / 256), block, 0, st, ctx->d_vals[1], K, per, Q, clen,
                                    ctx->d_cqueue);
-                // the other pixels in slot order: stable 1-bit partition by "is one of the K"
-                hipLaunchKernelGGL(k_flag_top, eg, block, 0, st, ctx->d_vals[1], n, K, ctx->d_keys[0]);
+                // the other pixels in slot order, the bulk's own costliest k*W of them first in a
+                // class of priority lanes (as on a small shard without the split): stable 2-bit
+                // partition rest | bulk priority | dedicated
+                const char* be = std::getenv("NART_RQ_SPLIT_BULKK");
+                const uint32_t kb = be ? (uint32_t)std::max(0, std::min(32, std::atoi(be))) : 8u;
+                const uint32_t nbulk = n - K, E = std::min(kb * W, nbulk / 2u);
+                hipLaunchKernelGGL(k_flag_classes, eg, block, 0, st, ctx->d_vals[1], n, K, E, ctx->d_keys[0]);
                 hipLaunchKernelGGL(k_iota, eg, block, 0, st, ctx->d_cost, n);
                 tmp = ctx->cap_sort_tmp;
                 HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->d_sort_tmp, tmp, ctx->d_keys[0], ctx->d_keys[1], ctx->d_cost,
-                                                          ctx->d_queue, (int)n, 0, 1, st));
+                                                          ctx->d_queue, (int)n, 0, 2, st));
+                uint32_t bq_len = nbulk, bpairs = 0;
+                const uint32_t* bq = ctx->d_queue;
+                if (E && kb && E == kb * W && (uint64_t)64u * W <= nbulk) {
+                    const int pe2 = std::getenv("NART_RQ_PAIRS") ? std::atoi(std::getenv("NART_RQ_PAIRS")) : NART_RQ_GROUP_LANES;
+                    const uint32_t Q2 = pe2 <= 0 ? 0u : (pe2 >= 4 ? 4u : 2u);
+                    bpairs = (Q2 && Q2 * kb <= 64u) ? Q2 : 0u;
+                    bq_len = nbulk + (bpairs ? (bpairs - 1u) * kb * W : 0u);
+                    hipLaunchKernelGGL(k_build_queue, dim3((bq_len + 255) / 256), block, 0, st, ctx->d_queue + (nbulk - E),
+                                       ctx->d_queue, nbulk, W, kb, RQ_PRIO_BIT, bpairs, ctx->d_keys[1]);
+                    bq = ctx->d_keys[1];
+                }
                 if (!ctx->st2) {
                     HIPCHK(hipStreamCreateWithFlags(&ctx->st2, hipStreamNonBlocking));
                     for (auto& e : ctx->ev_split) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -772,10 +811,10 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                 HIPCHK(hipGetLastError());
                 HIPCHK(hipEventRecord(ctx->ev_split[1], ctx->st2));
                 RenderArgs bb = b;
-                bb.queue = ctx->d_queue;
-                bb.qlen = n - K;
-                bb.rq_prio = 0u;
-                bb.rq_pairs = 0u;
+                bb.queue = bq;
+                bb.qlen = bq_len;
+                bb.rq_prio = bq != ctx->d_queue ? 1u : 0u;
+                bb.rq_pairs = bpairs;
                 HIPCHK(hipMemsetAsync(ctx->d_qhead, 0, sizeof(uint32_t), st));
                 bb.qhead = ctx->d_qhead;
                 const uint32_t perb = NART_RQ_BLOCK / 256;
@@ -871,6 +910,9 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     RenderArgs b = a;
     // small density grids (C5: 2x2x2) are read from LDS (NART_VOL_LDS=0: from global memory)
     const bool vol_lds = !(std::getenv("NART_VOL_LDS") && std::getenv("NART_VOL_LDS")[0] == '0');
+    // NART_VOL_BATCH (read per call): phase batching of the state machine (k_render_volume_sm)
+    const char* vb = std::getenv("NART_VOL_BATCH");
+    b.vol_batch = vb ? (uint32_t)std::max(0, std::atoi(vb)) : 0u;
     const uint32_t nd = ctx->scene.medium.present ? ctx->scene.medium.rx * ctx->scene.medium.ry * ctx->scene.medium.rz : 0;
     b.lds_nodes = (sm && vol_lds && nd <= 4096u) ? nd : 0u;
     const size_t dl = (size_t)b.lds_nodes * sizeof(float);
@@ -902,7 +944,7 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             // against 3 ms at the corners), so whole costly groups made waves of 64 long chains
             // (one 8x8 wave of them: 66 ms alone).  0: the costliest wave-sized groups first.
             const char* ke = std::getenv("NART_VOL_K");
-            const uint32_t k = std::min(64u, ke ? (uint32_t)std::max(0, std::atoi(ke)) : 2u);
+            const uint32_t k = std::min(64u, ke ? (uint32_t)std::max(0, std::atoi(ke)) : 0u);
             if (k == 0 || !sm || (uint64_t)k * W > n) {
                 rc = sort_groups_by_cost(ctx, n, ctx->d_queue, st);
                 if (rc) return rc;
@@ -921,15 +963,21 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                                                           ctx->d_vals[0], (int)n, 0, 1, st));
                 hipLaunchKernelGGL(k_build_queue, eg, block, 0, st, ctx->d_vals[1], ctx->d_vals[0], n, W, k, 0u, 0u,
                                    ctx->d_queue);
-                HIPCHK(hipMemsetAsync(ctx->d_qhead, 0, sizeof(uint32_t), st));
                 b.queue = ctx->d_queue;
-                b.qhead = ctx->d_qhead;
-                b.qlen = n;
-                int pc = 0;
-                HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                    &pc, w4 ? (const void*)k_render_volume_sm<false, 4> : (const void*)k_render_volume_sm<false, 1>, 256, dl));
-                grid = (uint32_t)std::max(1, cus * std::max(pc, 1));
-                b.qbase = grid * 256;
+                // NART_VOL_REFILL=1: persistent lanes taking the next queue entry (desynchronised
+                // lanes: every phase of the state machine runs in every iteration)
+                const char* fe = std::getenv("NART_VOL_REFILL");
+                if (fe && std::atoi(fe) != 0) {
+                    HIPCHK(hipMemsetAsync(ctx->d_qhead, 0, sizeof(uint32_t), st));
+                    b.qhead = ctx->d_qhead;
+                    b.qlen = n;
+                    int pc = 0;
+                    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                        &pc, w4 ? (const void*)k_render_volume_sm<false, 4> : (const void*)k_render_volume_sm<false, 1>, 256,
+                        dl));
+                    grid = (uint32_t)std::max(1, cus * std::max(pc, 1));
+                    b.qbase = grid * 256;
+                }
             }
             HIPCHK(hipGetLastError());
         }
@@ -1238,9 +1286,14 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
             const uint32_t pb = 64u / g.tile_size, nblk = (nbk * nb + 4 * pb - 1) / (4 * pb);
             const size_t lds = lut.size() * sizeof(float4) + 8u * pb * sizeof(uint32_t);
             const int fbk = (int)g.filter_bounds * 2 + (int)nb - 1;
+            // NART_SKEW_WAVES=4 (read per call): the build held to 4 waves per SIMD (<= 128 VGPRs)
+            const char* swe = std::getenv("NART_SKEW_WAVES");
+            const bool w4s = swe && std::atoi(swe) >= 4;
             if (fbk == 2) hipLaunchKernelGGL((k_splat_skew<1, 1>), dim3(nblk), dim3(256), lds, st, sa);
             else if (fbk == 3) hipLaunchKernelGGL((k_splat_skew<1, 2>), dim3(nblk), dim3(256), lds, st, sa);
+            else if (fbk == 4 && w4s) hipLaunchKernelGGL((k_splat_skew<2, 1, 4>), dim3(nblk), dim3(256), lds, st, sa);
             else if (fbk == 4) hipLaunchKernelGGL((k_splat_skew<2, 1>), dim3(nblk), dim3(256), lds, st, sa);
+            else if (fbk == 5 && w4s) hipLaunchKernelGGL((k_splat_skew<2, 2, 4>), dim3(nblk), dim3(256), lds, st, sa);
             else if (fbk == 5) hipLaunchKernelGGL((k_splat_skew<2, 2>), dim3(nblk), dim3(256), lds, st, sa);
             else if (fbk == 6) hipLaunchKernelGGL((k_splat_skew<3, 1>), dim3(nblk), dim3(256), lds, st, sa);
             else hipLaunchKernelGGL((k_splat_skew<3, 2>), dim3(nblk), dim3(256), lds, st, sa);

@@ -228,18 +228,39 @@ def test_volume_integrator(gpu, volume_scenes, kind):
     assert _bits_equal(g, r), _report(g, r)
 
 
-@pytest.mark.parametrize("k", ["2", "8", "0"], ids=["dealt-2", "dealt-8", "groups"])
+@pytest.mark.parametrize("k,refill", [("2", "0"), ("8", "1"), ("0", "0")], ids=["dealt-2", "dealt-8-refill", "groups"])
 @pytest.mark.parametrize("kind", ["c5", "emissive"])
-def test_volume_queue_scheduler(gpu, volume_scenes, monkeypatch, kind, k):
+def test_volume_queue_scheduler(gpu, volume_scenes, monkeypatch, kind, k, refill):
     """More pixels than resident lanes: the volume kernel runs its cost probe (4 samples per
-    pixel); the costliest single pixels are dealt k per wave over the first round of persistent
-    waves whose lanes refill from the queue (NART_VOL_K=0: the costliest pixel groups first, one
-    lane per pixel; render.hip dispatch_volume).  Only the order of work changes."""
+    pixel); the costliest single pixels are dealt k per wave over the first round of waves, whose
+    lanes optionally refill from the queue (NART_VOL_REFILL=1: persistent lanes), or the costliest
+    pixel groups run first (NART_VOL_K=0; render.hip dispatch_volume).  Only the order of work
+    changes."""
     monkeypatch.setenv("NART_VOL_K", k)
+    monkeypatch.setenv("NART_VOL_REFILL", refill)
     sc = volume_scenes[kind]
     p = _params(sc, 640, 360, 8)
     g = nart_amd.HipRenderer(sc).render(p)
     r = oracle.Oracle(sc).render(p)
+    assert _bits_equal(g, r), _report(g, r)
+
+
+@pytest.mark.parametrize("batch", ["2", "4", "16"])
+@pytest.mark.parametrize("kind", ["c5", "emissive"])
+def test_volume_phase_batching(gpu, volume_scenes, monkeypatch, kind, batch):
+    """Phase batching of the volume state machine (NART_VOL_BATCH=F: scatter directions, new
+    medium segments and escapes run once 1/F of a wave's lanes wait for them): only when each
+    lane's steps run changes, so frame (640x360, more pixels than resident lanes) and per-sample
+    results must equal the oracle's bit for bit."""
+    monkeypatch.setenv("NART_VOL_BATCH", batch)
+    sc = volume_scenes[kind]
+    p = _params(sc, 640, 360, 8)
+    g = nart_amd.HipRenderer(sc).render(p)
+    r = oracle.Oracle(sc).render(p)
+    assert _bits_equal(g, r), _report(g, r)
+    p = _params(sc, 320, 180, 32)
+    g = nart_amd.HipRenderer(sc).render_samples(p, 140, 70, 16, 12)
+    r = oracle.Oracle(sc).render_samples(p, 140, 70, 16, 12)
     assert _bits_equal(g, r), _report(g, r)
 
 
