@@ -119,9 +119,6 @@ struct RenderArgs {
     uint32_t* ghead = nullptr;
     // with ghead: the n-th group taken is gorder[n] (null: slot order)
     const uint32_t* gorder = nullptr;
-    // k_render_volume_sm phase batching: the rare, expensive phases run once >= 1/vol_batch of the
-    // wave's active lanes wait for them (0: every iteration)
-    uint32_t vol_batch = 0;
 };
 #define RQ_PRIO_BIT 0x80000000u
 #define RQ_PAIR_BIT 0x40000000u
@@ -2106,8 +2103,8 @@ __global__ __launch_bounds__(256) void k_splat_col4(SplatArgs A) {
 // lanes with its own source rows [band start - 2R, band end - 1] (the 2R rows before a band are
 // read by both neighbours): NB times the waves for ~1/NB of the steps each, for launches whose
 // time is otherwise the waves' latency (VALU ~30 % busy at 2.7 waves per SIMD).
-template <int R, int NB, int WV = 1>
-__global__ __launch_bounds__(256, WV) void k_splat_skew(SplatArgs A) {
+template <int R, int NB>
+__global__ __launch_bounds__(256) void k_splat_skew(SplatArgs A) {
     constexpr int W = 2 * R + 1, NWR = 2 * R + 2;
     extern __shared__ __attribute__((aligned(16))) float4 s_dyn4[];
     float4* s_lut = s_dyn4;

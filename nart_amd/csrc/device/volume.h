@@ -284,11 +284,10 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
     }
     __syncthreads();
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-    // with A.qhead the grid is persistent: a lane whose pixel is done takes the next queue entry
-    // (queue[qbase + atomicAdd(qhead)]) instead of idling until its wave ends
-    const uint32_t qlen = A.qlen ? A.qlen : A.n_slots;
-    if (gid >= (A.qhead ? qlen : A.n_slots)) return;
+    const uint32_t qlen = A.qlen ? A.qlen : A.n_slots;  // queue entries (sparse waves: > n_slots)
+    if (gid >= qlen) return;
     uint32_t slot = A.queue ? A.queue[gid] : gid;
+    if (slot == 0xFFFFFFFFu) return;  // an idle lane of a sparse wave (dispatch_volume)
     uint32_t px = 0, py = 0, rng = 0;
     SlotSO so;
     const float2* smp = nullptr;
@@ -315,26 +314,8 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
     MajIter it;
     for (;;) {
         bool finish = false;
-        // Phase batching (A.vol_batch = F): the wave executes the union of its lanes' phases, and
-        // the rare ones -- a scatter direction (acosf + 2 sinf/cosf), a new ray segment through the
-        // medium box, the escape to the lights -- cost several times a tentative collision.  They
-        // run only when at least 1/F of the wave's active lanes wait for one (or no lane has a
-        // cheap phase left); until then those lanes idle while the others keep sampling
-        // collisions.  Each lane's own operations and their order are unchanged.
-        bool xok = true;
-        if (A.vol_batch) {
-            const bool cheap = ph == P_SAMPLE || ph == P_MAJ || ph == P_COLL;
-            const uint64_t mc = __ballot(cheap), me = __ballot(!cheap);
-            xok = mc == 0 || (uint32_t)__popcll(me) * A.vol_batch >= (uint32_t)__popcll(mc | me);
-        }
         if (ph == P_SAMPLE) {
-            if (s >= A.spp) {
-                if (!A.qhead || A.cost) break;
-                const uint32_t idx = A.qbase + atomicAdd(A.qhead, 1u);
-                if (idx >= qlen) break;
-                take(A.queue[idx]);
-                s = 0;
-            }
+            if (s >= A.spp) break;
             const float2 sm = smp[(size_t)s * so.stride];
             const Ray r = cast_ray(S, F2(sm.x, sm.y), A.W, A.H, px, py);
             o = r.o;
@@ -343,13 +324,13 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
             bounce = 0;
             ph = P_RAY;
         }
-        if (ph == P_SCAT && xok) {  // isotropic scattering direction (volumeintegrator.cpp:44-47)
+        if (ph == P_SCAT) {  // isotropic scattering direction (volumeintegrator.cpp:44-47)
             const float a = rng_float(rng);
             const float b = rng_float(rng);
             d = uniform_sample_sphere(F2(a, b));
             ph = P_RAY;
         }
-        if (ph == P_RAY && xok) {  // top of VolumeIntegrator's bounce loop
+        if (ph == P_RAY) {  // top of VolumeIntegrator's bounce loop
             (void)rng_float(rng);  // u: passed to SampleT_maj, unused there
             uMode = rng_float(rng);
             if (m.present && medium_sample_ray(m, o, d, it)) {
@@ -424,7 +405,7 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
                 }
             }
         }
-        if (ph == P_ESC && xok) {
+        if (ph == P_ESC) {
             float lightTMax = __builtin_inff();
             f3 Le = F3(0.f, 0.f, 0.f);
             for (uint32_t j = 0; j < S.num_lights; ++j) {

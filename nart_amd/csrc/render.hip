@@ -76,10 +76,6 @@ struct nart_ctx {
     uint32_t* d_keys[2] = {nullptr, nullptr};
     uint32_t* d_vals[2] = {nullptr, nullptr};
     uint32_t* d_qhead = nullptr;
-    uint32_t* d_cqueue = nullptr;  // split launch: the costliest pixels' dedicated waves
-    uint32_t cap_cqueue = 0;
-    hipStream_t st2 = nullptr;     // split launch: second stream of the device
-    hipEvent_t ev_split[2] = {nullptr, nullptr};
     void* d_sort_tmp = nullptr;
     size_t cap_sort_tmp = 0;
     uint32_t cap_queue = 0;
@@ -528,31 +524,21 @@ __global__ void k_slot_rows(uint32_t n, uint32_t spp, SlotSO* so) {
     if (i < n) so[i] = SlotSO{(unsigned long long)i * spp, 1u, 0u};
 }
 
-// Sort keys of single pixels, costliest first (ascending sort of ~cost), values = slot ids.
-__global__ void k_cost_keys(const uint32_t* cost, uint32_t n, uint32_t* keys, uint32_t* vals) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    keys[i] = ~cost[i];
-    vals[i] = i;
-}
-
-// Split launch, classes of the cost-sorted pixels: 2 the K dedicated chains, 1 the next E (the
-// priority pixels of the bulk launch), 0 the rest.
-__global__ void k_flag_classes(const uint32_t* sorted, uint32_t n, uint32_t K, uint32_t E, uint32_t* flag) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n) return;
-    flag[sorted[r]] = r < K ? 2u : (r < K + E ? 1u : 0u);
-}
-
-// Split launch, the chains' queue: wave w holds chains w*per .. w*per+per-1 of the cost-sorted
-// list, chain c on the Q adjacent lanes (c % per)*Q .. +Q-1 (speculative lane group); every other
-// lane of the wave holds no pixel and only traces the wave's queued rays.
-__global__ void k_chain_queue(const uint32_t* sorted, uint32_t K, uint32_t per, uint32_t Q, uint32_t len,
-                              uint32_t* q) {
+// Volume queue with the H costliest groups (sorted group ids, costliest first) spread S pixels per
+// wave, the wave's other lanes idle (0xFFFFFFFF), then the remaining groups dense.
+__global__ void k_sparse_groups(const uint32_t* groups, uint32_t n, uint32_t H, uint32_t S, uint32_t qlen,
+                                uint32_t* queue) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= len) return;
-    const uint32_t w = p / 64u, j = p % 64u, c = w * per + j / Q;
-    q[p] = (j < per * Q && c < K) ? (sorted[c] | RQ_PRIO_BIT | (Q > 1u ? RQ_PAIR_BIT : 0u)) : 0xFFFFFFFFu;
+    if (p >= qlen) return;
+    const uint32_t hot = H * (64u / S) * 64u;
+    if (p < hot) {
+        const uint32_t w = p / 64u, j = p % 64u, g = w / (64u / S), part = w % (64u / S);
+        const uint32_t slot = 64u * groups[g] + part * S + j;
+        queue[p] = (j < S && slot < n) ? slot : 0xFFFFFFFFu;
+    } else {
+        const uint32_t r = p - hot + 64u * H;  // rank in the dense group order
+        queue[p] = 64u * groups[r / 64u] + r % 64u;
+    }
 }
 
 __global__ void k_iota(uint32_t* v, uint32_t n) {
@@ -577,22 +563,6 @@ int sort_groups_by_cost(nart_ctx* ctx, uint32_t n, uint32_t* out, hipStream_t st
                                               ctx->d_vals[1], (int)ng, 0, 32, st));
     hipLaunchKernelGGL(k_expand_groups, dim3((n + 255) / 256), dim3(256), 0, st, ctx->d_vals[1], n, out);
     HIPCHK(hipGetLastError());
-    return NART_OK;
-}
-
-// Radix-sort scratch for a 32-bit-key sort of n pairs (grown on demand; the stream is drained first
-// because the scratch may be in use by work already queued on it).
-int ensure_sort_tmp(nart_ctx* ctx, uint32_t n, hipStream_t st) {
-    size_t need = 0;
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, need, ctx->d_keys[0], ctx->d_keys[1], ctx->d_vals[0], ctx->d_vals[1],
-                                              (int)n, 0, 32));
-    if (need + 256 <= ctx->cap_sort_tmp) return NART_OK;
-    HIPCHK(hipStreamSynchronize(st));
-    if (ctx->d_sort_tmp) hipFree(ctx->d_sort_tmp);
-    ctx->d_sort_tmp = nullptr;
-    ctx->cap_sort_tmp = 0;
-    HIPCHK(hipMalloc(&ctx->d_sort_tmp, need + 256));
-    ctx->cap_sort_tmp = need + 256;
     return NART_OK;
 }
 
@@ -735,96 +705,6 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                 HIPCHK(hipGetLastError());
                 return NART_OK;
             }
-            // split launch (NART_RQ_SPLIT=K, read per call): the K costliest single pixels of the cost
-            // probe run as dedicated waves on a second stream (per chains of Q speculative lanes in
-            // each, the other lanes only tracing their rays), so that their serial chains see
-            // little contention; the other pixels fill the device from a slot-order refill queue
-            const char* se = std::getenv("NART_RQ_SPLIT");
-            uint32_t K = se ? (uint32_t)std::max(0, std::atoi(se)) : 0u;
-            if (rq && mode == 2 && K > 0 && R < q_rounds) {
-                const char* qe = std::getenv("NART_RQ_SPLIT_Q");
-                const char* pe = std::getenv("NART_RQ_SPLIT_PER");
-                const char* ps = std::getenv("NART_RQ_SPLIT_PROBE");
-                const uint32_t Q = qe ? (std::atoi(qe) >= 4 ? 4u : (std::atoi(qe) >= 2 ? 2u : 1u)) : 4u;
-                const uint32_t per = std::max(1u, std::min(64u / Q, pe ? (uint32_t)std::atoi(pe) : 1u));
-                const uint32_t pspp = std::max(1u, std::min(a.spp, ps ? (uint32_t)std::atoi(ps) : 1u));
-                K = std::min(K, n / 2u);
-                const uint32_t Wc = (K + per - 1u) / per, clen = Wc * 64u;
-                RenderArgs pb = b;  // cost probe: the first pspp samples of every pixel
-                pb.spp = pspp;
-                pb.cost = ctx->d_cost;
-                hipLaunchKernelGGL((k_render<MAXL, true, ENV, false>), dim3(blocks), block, lds, st, ctx->scene, pb);
-                hipLaunchKernelGGL(k_cost_keys, eg, block, 0, st, ctx->d_cost, n, ctx->d_keys[0], ctx->d_vals[0]);
-                if (int rc3 = ensure_sort_tmp(ctx, n, st)) return rc3;
-                size_t tmp = ctx->cap_sort_tmp;
-                HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->d_sort_tmp, tmp, ctx->d_keys[0], ctx->d_keys[1],
-                                                          ctx->d_vals[0], ctx->d_vals[1], (int)n, 0, 32, st));
-                if (clen > ctx->cap_cqueue) {
-                    HIPCHK(hipStreamSynchronize(st));
-                    if (ctx->d_cqueue) hipFree(ctx->d_cqueue);
-                    ctx->d_cqueue = nullptr;
-                    ctx->cap_cqueue = 0;
-                    HIPCHK(hipMalloc(&ctx->d_cqueue, (size_t)clen * 4));
-                    ctx->cap_cqueue = clen;
-                }
-                hipLaunchKernelGGL(k_chain_queue, dim3((clen + 255) / 256), block, 0, st, ctx->d_vals[1], K, per, Q, clen,
-                                   ctx->d_cqueue);
-                // the other pixels in slot order, the bulk's own costliest k*W of them first in a
-                // class of priority lanes (as on a small shard without the split): stable 2-bit
-                // partition rest | bulk priority | dedicated
-                const char* be = std::getenv("NART_RQ_SPLIT_BULKK");
-                const uint32_t kb = be ? (uint32_t)std::max(0, std::min(32, std::atoi(be))) : 8u;
-                const uint32_t nbulk = n - K, E = std::min(kb * W, nbulk / 2u);
-                hipLaunchKernelGGL(k_flag_classes, eg, block, 0, st, ctx->d_vals[1], n, K, E, ctx->d_keys[0]);
-                hipLaunchKernelGGL(k_iota, eg, block, 0, st, ctx->d_cost, n);
-                tmp = ctx->cap_sort_tmp;
-                HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->d_sort_tmp, tmp, ctx->d_keys[0], ctx->d_keys[1], ctx->d_cost,
-                                                          ctx->d_queue, (int)n, 0, 2, st));
-                uint32_t bq_len = nbulk, bpairs = 0;
-                const uint32_t* bq = ctx->d_queue;
-                if (E && kb && E == kb * W && (uint64_t)64u * W <= nbulk) {
-                    const int pe2 = std::getenv("NART_RQ_PAIRS") ? std::atoi(std::getenv("NART_RQ_PAIRS")) : NART_RQ_GROUP_LANES;
-                    const uint32_t Q2 = pe2 <= 0 ? 0u : (pe2 >= 4 ? 4u : 2u);
-                    bpairs = (Q2 && Q2 * kb <= 64u) ? Q2 : 0u;
-                    bq_len = nbulk + (bpairs ? (bpairs - 1u) * kb * W : 0u);
-                    hipLaunchKernelGGL(k_build_queue, dim3((bq_len + 255) / 256), block, 0, st, ctx->d_queue + (nbulk - E),
-                                       ctx->d_queue, nbulk, W, kb, RQ_PRIO_BIT, bpairs, ctx->d_keys[1]);
-                    bq = ctx->d_keys[1];
-                }
-                if (!ctx->st2) {
-                    HIPCHK(hipStreamCreateWithFlags(&ctx->st2, hipStreamNonBlocking));
-                    for (auto& e : ctx->ev_split) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-                }
-                HIPCHK(hipEventRecord(ctx->ev_split[0], st));
-                HIPCHK(hipStreamWaitEvent(ctx->st2, ctx->ev_split[0], 0));
-                RenderArgs c = b;
-                c.queue = ctx->d_cqueue;
-                c.qlen = clen;
-                c.qhead = nullptr;
-                c.rq_prio = 1u;
-                c.rq_pairs = Q > 1u ? Q : 0u;
-                c.rq_quorum = 0u;
-                c.lds_nodes = brq.lds_nodes;
-                c.prim = brq.prim;
-                hipLaunchKernelGGL(kern_rq, dim3((clen + NART_RQ_BLOCK - 1) / NART_RQ_BLOCK), dim3(NART_RQ_BLOCK), lds_rq,
-                                   ctx->st2, ctx->scene, c);
-                HIPCHK(hipGetLastError());
-                HIPCHK(hipEventRecord(ctx->ev_split[1], ctx->st2));
-                RenderArgs bb = b;
-                bb.queue = bq;
-                bb.qlen = bq_len;
-                bb.rq_prio = bq != ctx->d_queue ? 1u : 0u;
-                bb.rq_pairs = bpairs;
-                HIPCHK(hipMemsetAsync(ctx->d_qhead, 0, sizeof(uint32_t), st));
-                bb.qhead = ctx->d_qhead;
-                const uint32_t perb = NART_RQ_BLOCK / 256;
-                const uint32_t bblocks = (resident + perb - 1u) / perb * perb;
-                bb.qbase = bblocks * 256;
-                launch(bblocks, bb);
-                HIPCHK(hipGetLastError());
-                HIPCHK(hipStreamWaitEvent(st, ctx->ev_split[1], 0));
-                return NART_OK;
-            }
             if (const char* e = std::getenv("NART_QUEUE_K")) k = (uint32_t)std::max(1, std::min(64, std::atoi(e)));
             const bool refill = k < 64u || mode == 1;
             if (mode == 1) {
@@ -910,9 +790,6 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     RenderArgs b = a;
     // small density grids (C5: 2x2x2) are read from LDS (NART_VOL_LDS=0: from global memory)
     const bool vol_lds = !(std::getenv("NART_VOL_LDS") && std::getenv("NART_VOL_LDS")[0] == '0');
-    // NART_VOL_BATCH (read per call): phase batching of the state machine (k_render_volume_sm)
-    const char* vb = std::getenv("NART_VOL_BATCH");
-    b.vol_batch = vb ? (uint32_t)std::max(0, std::atoi(vb)) : 0u;
     const uint32_t nd = ctx->scene.medium.present ? ctx->scene.medium.rx * ctx->scene.medium.ry * ctx->scene.medium.rz : 0;
     b.lds_nodes = (sm && vol_lds && nd <= 4096u) ? nd : 0u;
     const size_t dl = (size_t)b.lds_nodes * sizeof(float);
@@ -938,45 +815,42 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             pb.cost = ctx->d_cost;
             if (sm) hipLaunchKernelGGL((k_render_volume_sm<false, 1>), dim3(blocks), block, dl, st, ctx->scene, pb);
             else hipLaunchKernelGGL((k_render_volume<false>), dim3(blocks), block, 0, st, ctx->scene, pb);
-            // NART_VOL_K (read per call): costly pixels dealt to each wave of the first round, the
-            // waves persistent (a lane whose pixel is done takes the next queue entry).  A frame's
-            // costliest volume pixels cluster (C5: the image centre, 32 ms alone at 1,024 spp
-            // against 3 ms at the corners), so whole costly groups made waves of 64 long chains
-            // (one 8x8 wave of them: 66 ms alone).  0: the costliest wave-sized groups first.
-            const char* ke = std::getenv("NART_VOL_K");
-            const uint32_t k = std::min(64u, ke ? (uint32_t)std::max(0, std::atoi(ke)) : 0u);
-            if (k == 0 || !sm || (uint64_t)k * W > n) {
-                rc = sort_groups_by_cost(ctx, n, ctx->d_queue, st);
-                if (rc) return rc;
-                b.queue = ctx->d_queue;
-            } else {
-                const dim3 eg((n + 255) / 256);
-                hipLaunchKernelGGL(k_cost_keys, eg, block, 0, st, ctx->d_cost, n, ctx->d_keys[0], ctx->d_vals[0]);
-                if ((rc = ensure_sort_tmp(ctx, n, st))) return rc;
-                size_t tmp = ctx->cap_sort_tmp;
-                HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->d_sort_tmp, tmp, ctx->d_keys[0], ctx->d_keys[1],
-                                                          ctx->d_vals[0], ctx->d_vals[1], (int)n, 0, 32, st));
-                hipLaunchKernelGGL(k_flag_top, eg, block, 0, st, ctx->d_vals[1], n, k * W, ctx->d_keys[0]);
-                hipLaunchKernelGGL(k_iota, eg, block, 0, st, ctx->d_cost, n);
-                tmp = ctx->cap_sort_tmp;
-                HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->d_sort_tmp, tmp, ctx->d_keys[0], ctx->d_keys[1], ctx->d_cost,
-                                                          ctx->d_vals[0], (int)n, 0, 1, st));
-                hipLaunchKernelGGL(k_build_queue, eg, block, 0, st, ctx->d_vals[1], ctx->d_vals[0], n, W, k, 0u, 0u,
-                                   ctx->d_queue);
-                b.queue = ctx->d_queue;
-                // NART_VOL_REFILL=1: persistent lanes taking the next queue entry (desynchronised
-                // lanes: every phase of the state machine runs in every iteration)
-                const char* fe = std::getenv("NART_VOL_REFILL");
-                if (fe && std::atoi(fe) != 0) {
-                    HIPCHK(hipMemsetAsync(ctx->d_qhead, 0, sizeof(uint32_t), st));
-                    b.qhead = ctx->d_qhead;
-                    b.qlen = n;
-                    int pc = 0;
-                    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                        &pc, w4 ? (const void*)k_render_volume_sm<false, 4> : (const void*)k_render_volume_sm<false, 1>, 256,
-                        dl));
-                    grid = (uint32_t)std::max(1, cus * std::max(pc, 1));
-                    b.qbase = grid * 256;
+            rc = sort_groups_by_cost(ctx, n, ctx->d_queue, st);
+            if (rc) return rc;
+            b.queue = ctx->d_queue;
+            // Sparse waves on shards of < NART_VOL_SPARSE_ROUNDS (default 2) rounds of resident
+            // waves: the costliest groups (probe cost >= NART_VOL_SPARSE_F (4) x the median group's)
+            // spread NART_VOL_SPARSE (16) pixels per wave, the other lanes idle.  A wave executes
+            // the union of its lanes' divergent chains, and a frame's costliest volume pixels
+            // cluster: C5's centre pixels take 30 ms alone at 1,024 spp, 69 ms as a wave of 64.
+            // C5 1/8 shard 73.7 -> 65.3 ms; on larger shards (2+ rounds) the mostly idle sparse
+            // waves hold slots the other groups need (1/2 shard 78 -> 127 ms), and 1-8 pixels per
+            // wave measured worse (profiles/r04h_c5_sparse.log).  Only the order of work changes.
+            const char* se = std::getenv("NART_VOL_SPARSE");
+            const char* fe = std::getenv("NART_VOL_SPARSE_F");
+            const char* re = std::getenv("NART_VOL_SPARSE_ROUNDS");
+            const uint32_t S = se ? std::max(1u, std::min(64u, (uint32_t)std::atoi(se))) : 16u;
+            const double f = fe ? std::atof(fe) : 4.0, max_rounds = re ? std::atof(re) : 2.0;
+            if (sm && S < 64u && (64u % S) == 0u && (double)blocks / (double)resident < max_rounds) {
+                const uint32_t ng = (n + 63) / 64;
+                std::vector<uint32_t> keys(ng);
+                HIPCHK(hipMemcpyAsync(keys.data(), ctx->d_keys[1], (size_t)ng * 4, hipMemcpyDeviceToHost, st));
+                HIPCHK(hipStreamSynchronize(st));
+                std::vector<uint32_t> costs;  // sorted descending (partial last group excluded)
+                for (uint32_t g = 0; g < ng; ++g)
+                    if (keys[g] != 0xFFFFFFFFu) costs.push_back(0xFFFFFFFEu - keys[g]);
+                uint32_t H = 0;
+                if (!costs.empty()) {
+                    const double med = costs[costs.size() / 2];
+                    while (H < costs.size() && (double)costs[H] >= f * med) ++H;
+                }
+                H = std::min<uint32_t>(H, 63u * W / (64u / S * 64u));  // queue room (ensure_queue)
+                if (H) {
+                    const uint32_t qlen = H * (64u / S) * 64u + (n - 64u * H);
+                    hipLaunchKernelGGL(k_sparse_groups, dim3((qlen + 255) / 256), block, 0, st, ctx->d_vals[1], n, H, S,
+                                       qlen, ctx->d_queue);
+                    b.qlen = qlen;
+                    grid = (qlen + 255) / 256;
                 }
             }
             HIPCHK(hipGetLastError());
@@ -1286,14 +1160,9 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
             const uint32_t pb = 64u / g.tile_size, nblk = (nbk * nb + 4 * pb - 1) / (4 * pb);
             const size_t lds = lut.size() * sizeof(float4) + 8u * pb * sizeof(uint32_t);
             const int fbk = (int)g.filter_bounds * 2 + (int)nb - 1;
-            // NART_SKEW_WAVES=4 (read per call): the build held to 4 waves per SIMD (<= 128 VGPRs)
-            const char* swe = std::getenv("NART_SKEW_WAVES");
-            const bool w4s = swe && std::atoi(swe) >= 4;
             if (fbk == 2) hipLaunchKernelGGL((k_splat_skew<1, 1>), dim3(nblk), dim3(256), lds, st, sa);
             else if (fbk == 3) hipLaunchKernelGGL((k_splat_skew<1, 2>), dim3(nblk), dim3(256), lds, st, sa);
-            else if (fbk == 4 && w4s) hipLaunchKernelGGL((k_splat_skew<2, 1, 4>), dim3(nblk), dim3(256), lds, st, sa);
             else if (fbk == 4) hipLaunchKernelGGL((k_splat_skew<2, 1>), dim3(nblk), dim3(256), lds, st, sa);
-            else if (fbk == 5 && w4s) hipLaunchKernelGGL((k_splat_skew<2, 2, 4>), dim3(nblk), dim3(256), lds, st, sa);
             else if (fbk == 5) hipLaunchKernelGGL((k_splat_skew<2, 2>), dim3(nblk), dim3(256), lds, st, sa);
             else if (fbk == 6) hipLaunchKernelGGL((k_splat_skew<3, 1>), dim3(nblk), dim3(256), lds, st, sa);
             else hipLaunchKernelGGL((k_splat_skew<3, 2>), dim3(nblk), dim3(256), lds, st, sa);
@@ -1765,13 +1634,9 @@ void nart_hip_destroy(nart_ctx* ctx) {
                     ctx->d_L, ctx->d_bucket_ids, ctx->d_bucket_base, ctx->d_table, ctx->d_lut, ctx->d_counters, ctx->d_envs, ctx->d_density,
                     ctx->d_oc_nodes, ctx->d_oc_chunks, ctx->d_oc_tris, ctx->d_tri_leaf, ctx->d_oc_lock, ctx->d_oc_heap,
                     ctx->d_queue, ctx->d_cost, ctx->d_keys[0], ctx->d_keys[1], ctx->d_vals[0], ctx->d_vals[1],
-                    ctx->d_qhead, ctx->d_sort_tmp, ctx->d_cqueue};
+                    ctx->d_qhead, ctx->d_sort_tmp};
     for (void* b : bufs)
         if (b) hipFree(b);
-    if (ctx->st2) {
-        hipStreamDestroy(ctx->st2);
-        for (auto& e : ctx->ev_split) hipEventDestroy(e);
-    }
     for (void* b : ctx->env_bufs) hipFree(b);
     if (ctx->events)
         for (auto& e : ctx->ev) hipEventDestroy(e);

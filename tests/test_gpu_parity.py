@@ -120,22 +120,6 @@ def test_queue_speculative_pairs(gpu, glass_scene, monkeypatch, pairs):
     assert _bits_equal(g, r), _report(g, r)
 
 
-@pytest.mark.parametrize("k,q,per", [("300", "4", "1"), ("300", "2", "2"), ("200", "1", "4")],
-                         ids=["quads-1", "pairs-2", "single-4"])
-def test_split_launch_chains(gpu, glass_scene, monkeypatch, k, q, per):
-    """Split launch of a small shard: the k costliest pixels of the cost probe as dedicated waves
-    (per chains of q speculative lanes each) on a second stream, the rest from a slot-order
-    refill queue on the caller's stream.  Only where and when each pixel's chain runs changes;
-    the frame must equal the oracle's bit for bit."""
-    monkeypatch.setenv("NART_RQ_SPLIT", k)
-    monkeypatch.setenv("NART_RQ_SPLIT_Q", q)
-    monkeypatch.setenv("NART_RQ_SPLIT_PER", per)
-    p = _params(glass_scene, 512, 300, 24)
-    g = nart_amd.HipRenderer(glass_scene, variant=0).render(p)
-    r = oracle.Oracle(glass_scene).render(p)
-    assert _bits_equal(g, r), _report(g, r)
-
-
 @pytest.fixture(scope="module")
 def full_frame_1spp(glass_scene):
     """The C3 frame size at 1 spp: ~16 rounds of resident waves, so the ray-queue kernel runs its
@@ -228,39 +212,21 @@ def test_volume_integrator(gpu, volume_scenes, kind):
     assert _bits_equal(g, r), _report(g, r)
 
 
-@pytest.mark.parametrize("k,refill", [("2", "0"), ("8", "1"), ("0", "0")], ids=["dealt-2", "dealt-8-refill", "groups"])
+@pytest.mark.parametrize("sparse,rounds", [("64", "2"), ("16", "8"), ("4", "8")],
+                         ids=["groups", "sparse16", "sparse4"])
 @pytest.mark.parametrize("kind", ["c5", "emissive"])
-def test_volume_queue_scheduler(gpu, volume_scenes, monkeypatch, kind, k, refill):
+def test_volume_queue_scheduler(gpu, volume_scenes, monkeypatch, kind, sparse, rounds):
     """More pixels than resident lanes: the volume kernel runs its cost probe (4 samples per
-    pixel); the costliest single pixels are dealt k per wave over the first round of waves, whose
-    lanes optionally refill from the queue (NART_VOL_REFILL=1: persistent lanes), or the costliest
-    pixel groups run first (NART_VOL_K=0; render.hip dispatch_volume).  Only the order of work
-    changes."""
-    monkeypatch.setenv("NART_VOL_K", k)
-    monkeypatch.setenv("NART_VOL_REFILL", refill)
+    pixel) and launches the costliest pixel groups first; on small shards the costliest groups run
+    as sparse waves (NART_VOL_SPARSE pixels per wave, the other lanes idle; render.hip
+    dispatch_volume).  Only the order of work changes."""
+    monkeypatch.setenv("NART_VOL_SPARSE", sparse)
+    monkeypatch.setenv("NART_VOL_SPARSE_ROUNDS", rounds)
+    monkeypatch.setenv("NART_VOL_SPARSE_F", "1.1")  # some groups of this small frame count as costly
     sc = volume_scenes[kind]
     p = _params(sc, 640, 360, 8)
     g = nart_amd.HipRenderer(sc).render(p)
     r = oracle.Oracle(sc).render(p)
-    assert _bits_equal(g, r), _report(g, r)
-
-
-@pytest.mark.parametrize("batch", ["2", "4", "16"])
-@pytest.mark.parametrize("kind", ["c5", "emissive"])
-def test_volume_phase_batching(gpu, volume_scenes, monkeypatch, kind, batch):
-    """Phase batching of the volume state machine (NART_VOL_BATCH=F: scatter directions, new
-    medium segments and escapes run once 1/F of a wave's lanes wait for them): only when each
-    lane's steps run changes, so frame (640x360, more pixels than resident lanes) and per-sample
-    results must equal the oracle's bit for bit."""
-    monkeypatch.setenv("NART_VOL_BATCH", batch)
-    sc = volume_scenes[kind]
-    p = _params(sc, 640, 360, 8)
-    g = nart_amd.HipRenderer(sc).render(p)
-    r = oracle.Oracle(sc).render(p)
-    assert _bits_equal(g, r), _report(g, r)
-    p = _params(sc, 320, 180, 32)
-    g = nart_amd.HipRenderer(sc).render_samples(p, 140, 70, 16, 12)
-    r = oracle.Oracle(sc).render_samples(p, 140, 70, 16, 12)
     assert _bits_equal(g, r), _report(g, r)
 
 
