@@ -1102,7 +1102,11 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
     uint32_t jfl = 0, jst = 0, jend = 0, nd = 0, pF = 0, pR = 0, bm = 0;
     float4 jres = make_float4(0.f, 0.f, 0.f, 0.f);
     enum { J_VER = 1, J_FIN = 2, J_DOOM = 4 };
+    // the lane's next sample and camera hit, read with the current one (c_s: its index, or none)
+    uint32_t c_s = 0xFFFFFFFFu, c_prim = NO_HIT;
+    float2 c_sm = make_float2(0.f, 0.f);
     auto take_pixel = [&](uint32_t sl) {
+        c_s = 0xFFFFFFFFu;
         prio = A.rq_prio && (sl & RQ_PRIO_BIT);
         pm = A.rq_pairs && (sl & RQ_PAIR_BIT);
         if (A.rq_prio) sl &= ~(RQ_PRIO_BIT | RQ_PAIR_BIT);
@@ -1415,7 +1419,32 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
         //    a hit is to be shaded, a ray is queued or the pixel is done.
         while (active) {
             nd = 0;
-            const float2 sm = A.samples[soff + (uint64_t)s * sstr];
+            // pixel-major rows (stride 1): samples and camera hits are read in pairs, the odd one
+            // kept for the lane's next sample -- each read of a line the lane's neighbours do not
+            // share then serves two samples
+            float2 sm;
+            uint32_t gprim = NO_HIT;
+            {
+                const uint64_t si = soff + (uint64_t)s * sstr;
+                // (not in the environment-light build, whose registers are already spilling)
+                if (!ENV && s == c_s) {
+                    sm = c_sm;
+                    gprim = c_prim;
+                } else if (!ENV && sstr == 1u && (si & 1u) == 0u && s + 1u < A.spp) {
+                    const float4 q = reinterpret_cast<const float4*>(A.samples)[si >> 1];
+                    sm = make_float2(q.x, q.y);
+                    c_sm = make_float2(q.z, q.w);
+                    if (A.prim) {
+                        const uint2 h = reinterpret_cast<const uint2*>(A.prim)[si >> 1];
+                        gprim = h.x;
+                        c_prim = h.y;
+                    }
+                    c_s = s + 1u;
+                } else {
+                    sm = A.samples[si];
+                    if (A.prim) gprim = A.prim[si];
+                }
+            }
             const Ray ray = cast_ray(S, F2(sm.x, sm.y), A.W, A.H, px, py);
             L = F3(0.f, 0.f, 0.f);
             alpha = 0.f;
@@ -1436,7 +1465,7 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
             if (A.prim) {
                 // camera ray traced by k_primary: shade its hit in this phase
                 const float t = light_loop(ray.o, ray.d);
-                const uint32_t g = A.prim[soff + (uint64_t)s * sstr];
+                const uint32_t g = gprim;
                 if (g == NO_HIT) {
                     if (lightHit) L = Le;
                     end_sample(make_float4(L.x, L.y, L.z, alpha));
