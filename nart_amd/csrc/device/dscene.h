@@ -70,7 +70,12 @@ struct DEnvDist {
     uint32_t w, h;
     float invW, invH;
     const float *mpdf, *cpdf, *mcdf, *ccdf;
+    // guide tables of the two CDF searches (build_env; null: full searches): cell c of K (values
+    // in [c/K, (c+1)/K)) holds a | b << 16, the range of BinarySearch's upper bound, relative to
+    // the search start -- mguide[K] for the marginal, cguide[row * K + c] for the conditionals
+    const uint32_t *mguide, *cguide;
 };
+#define NART_ENV_GUIDE_K 64u
 
 struct DMesh {
     uint32_t material;

@@ -40,6 +40,21 @@ ND f3 light_li(const DScene& S, const DLight& L, f3 p, f3 wi, float* pdf, float&
     return F3(0.f, 0.f, 0.f);
 }
 
+// The light loop of an extension ray (pathintegrator.cpp:171-182) when its Le cannot reach L: Le
+// is used only when the camera ray escapes (pathintegrator.cpp:252-256, Q7), so for every other
+// ray the loop needs just the bound tMax (and whether it was lowered), which this sets exactly as
+// light_li does -- without the radiance: for the environment light the acosf / atan2f and the
+// texture fetch, a dependent global load.
+template <bool ENV = true>
+ND void light_bound(const DLight& L, f3 p, f3 wi, float& tMax) {
+    if (ENV && L.type == NART_LIGHT_ENVIRONMENT) {
+        tMax = ENV_TMAX;
+        return;
+    }
+    f2 st = F2(0.f, 0.f);
+    (void)area_pdf(L, p, wi, st, tMax);
+}
+
 // Light::Sample_Li (disklight.cpp:25-60, ringlight.cpp:130-168)
 template <bool ENV = true>
 ND f3 light_sample_li(const DScene& S, const DLight& L, f3 p, f3& wi, f2 sample, float& pdf, float& tMax) {

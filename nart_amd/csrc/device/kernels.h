@@ -662,15 +662,21 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
             float lightTMax = __builtin_inff();
             lightHit = false;
             Le = F3(0.f, 0.f, 0.f);
+            uint32_t lwin = 0;
             for (uint32_t j = 0; j < S.num_lights; ++j) {
                 float lt = __builtin_inff();
-                f3 Li = light_li<ENV>(S, S.lights[j], ray.o, ray.d, nullptr, lt);
+                light_bound<ENV>(S.lights[j], ray.o, ray.d, lt);
                 if (lt < lightTMax) {
-                    Le = Li;
                     lightTMax = lt;
                     lightHit = true;
                     alpha = 1.f;
+                    lwin = j;
                 }
+            }
+            // Le (the radiance of the light that set the bound) only matters for the camera ray
+            if (bounce == 0 && lightHit) {
+                float lt = __builtin_inff();
+                Le = light_li<ENV>(S, S.lights[lwin], ray.o, ray.d, nullptr, lt);
             }
             cur = ray;
             tmax = lightTMax;
@@ -951,7 +957,7 @@ __global__ __launch_bounds__(256) void k_primary(DScene S, RenderArgs A, uint32_
         float lightTMax = __builtin_inff();
         for (uint32_t j = 0; j < S.num_lights; ++j) {
             float lt = __builtin_inff();
-            light_li<ENV>(S, S.lights[j], ray.o, ray.d, nullptr, lt);
+            light_bound<ENV>(S.lights[j], ray.o, ray.d, lt);  // only the bound: no radiance
             if (lt < lightTMax) lightTMax = lt;
         }
         float bt;
@@ -1136,7 +1142,7 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
 
     TraceCounters cnt = {0u, 0u, 0u, 0u};
     uint32_t n_ext = 0, n_sh = 0, n_bounce = 0;
-    f3 L = F3(0.f, 0.f, 0.f), beta = F3(0.f, 0.f, 0.f), Le = F3(0.f, 0.f, 0.f);
+    f3 L = F3(0.f, 0.f, 0.f), beta = F3(0.f, 0.f, 0.f);
     f3 c1 = F3(0.f, 0.f, 0.f), c2 = F3(0.f, 0.f, 0.f), betak = F3(0.f, 0.f, 0.f);
     float alpha = 0.f, eta_sampled = 1.f, eta_outer = 1.f, alphaTweak = 1.f;
     uint32_t flags = 0, bounce = 0;
@@ -1178,21 +1184,30 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
     };
     // light intersections of a new extension ray (pathintegrator.cpp:167-182): Le, lightHit,
     // alpha; returns the query bound
+    // The loop keeps only the bound and the index of the light that set it (lwin): the radiance Le
+    // of that light reaches L only when the camera ray escapes (pathintegrator.cpp:252-256, Q7),
+    // and light_le evaluates it then -- the same light_li of the same ray, so the same Le -- instead
+    // of evaluating every light's radiance on every ray (the environment light: acosf + atan2f +
+    // a texture fetch).
+    uint32_t lwin = 0;
     auto light_loop = [&](f3 o, f3 d) {
         float lightTMax = __builtin_inff();
         lightHit = false;
-        Le = F3(0.f, 0.f, 0.f);
         for (uint32_t j = 0; j < S.num_lights; ++j) {
             float lt = __builtin_inff();
-            f3 Li = light_li<ENV>(S, S.lights[j], o, d, nullptr, lt);
+            light_bound<ENV>(S.lights[j], o, d, lt);
             if (lt < lightTMax) {
-                Le = Li;
                 lightTMax = lt;
                 lightHit = true;
                 alpha = 1.f;
+                lwin = j;
             }
         }
         return lightTMax;
+    };
+    auto light_le = [&](f3 o, f3 d) {
+        float lt = __builtin_inff();
+        return light_li<ENV>(S, S.lights[lwin], o, d, nullptr, lt);
     };
     auto draw = [&]() {
         ++nd;
@@ -1247,7 +1262,11 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                     hitg = r.x;
                 } else {
                     // escaped (at bounce 0 the light seen directly is the result, Q6, Q7) or ended
-                    if (ext_pending && bounce == 0 && lightHit) L = Le;
+                    if (ext_pending && bounce == 0 && lightHit) {
+                        // the camera ray, still in this lane's outbox entry of kind 0
+                        const float4 ro = my_out[lane * 2], rd = my_out[lane * 2 + 1];
+                        L = light_le(F3(ro.x, ro.y, ro.z), F3(rd.x, rd.y, rd.z));
+                    }
                     end_sample(make_float4(L.x, L.y, L.z, alpha));
                 }
                 }
@@ -1464,10 +1483,10 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
             }
             if (A.prim) {
                 // camera ray traced by k_primary: shade its hit in this phase
-                const float t = light_loop(ray.o, ray.d);
                 const uint32_t g = gprim;
+                const float t = light_loop(ray.o, ray.d);
                 if (g == NO_HIT) {
-                    if (lightHit) L = Le;
+                    if (lightHit) L = light_le(ray.o, ray.d);
                     end_sample(make_float4(L.x, L.y, L.z, alpha));
                     active = !pm && s < A.spp;
                     continue;

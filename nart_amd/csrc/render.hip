@@ -214,13 +214,42 @@ int build_env(nart_ctx* ctx, const nart_texture& t, DEnvDist& d) {
     for (uint32_t j = 0; j < H; ++j)
         for (uint32_t i = 1; i < W; ++i)
             ccdf[(size_t)j * (W + 1) + i] = ccdf[(size_t)j * (W + 1) + i - 1] + (cpdf[(size_t)j * W + i - 1] * invW);
-    void* bufs[4] = {nullptr, nullptr, nullptr, nullptr};
+    // guide tables of the two searches (path.h guided_search): per cell of values [c/K, (c+1)/K)
+    // the range [ub(c/K), ub(last float of the cell)] of the upper bound; built only over searched
+    // ranges that are non-decreasing and NaN-free (otherwise the full search runs)
+    const uint32_t K = NART_ENV_GUIDE_K;
+    auto guide = [&](const float* v, uint32_t n, uint32_t* out) {
+        for (uint32_t j = 0; j + 1 < n; ++j)
+            if (!(v[j] <= v[j + 1])) return false;
+        if (n && v[0] != v[0]) return false;
+        auto ub = [&](float x) { return (uint32_t)(std::upper_bound(v, v + n, x) - v); };
+        for (uint32_t c = 0; c < K; ++c) {
+            const float lo = (float)c / (float)K;
+            const float hi = c + 1 == K ? INFINITY : std::nextafter((float)(c + 1) / (float)K, 0.f);
+            out[c] = ub(lo) | (ub(hi) << 16);
+        }
+        return true;
+    };
+    std::vector<uint32_t> mguide(K), cguide((size_t)K * H);
+    bool guided = W <= 65535 && H <= 65535 && guide(mcdf.data(), H, mguide.data());
+    for (uint32_t j = 0; guided && j < H; ++j) guided = guide(ccdf.data() + (size_t)j * (W + 1), W, cguide.data() + (size_t)j * K);
+    void* bufs[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     const std::vector<float>* src[4] = {&mpdf, &cpdf, &mcdf, &ccdf};
     for (int k = 0; k < 4; ++k) {
         int rc = upload(ctx, bufs[k], src[k]->data(), src[k]->size());
         if (bufs[k]) ctx->env_bufs.push_back(bufs[k]);
         if (rc) return rc;
     }
+    if (guided) {
+        for (int k = 4; k < 6; ++k) {
+            const std::vector<uint32_t>& g = k == 4 ? mguide : cguide;
+            int rc = upload(ctx, bufs[k], g.data(), g.size());
+            if (bufs[k]) ctx->env_bufs.push_back(bufs[k]);
+            if (rc) return rc;
+        }
+    }
+    d.mguide = (const uint32_t*)bufs[4];
+    d.cguide = (const uint32_t*)bufs[5];
     d.w = W;
     d.h = H;
     d.invW = invW;
