@@ -1197,7 +1197,14 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
             else hipLaunchKernelGGL((k_splat_skew<3, 2>), dim3(nblk), dim3(256), lds, st, sa);
         } else if (sa.thr && sa.invB != 0.f && splat_mode >= 3)
         {
-            if (sa.lut)
+            // NART_COL4_NP=2 (read per call, A/B): two tile pixels per lane -- twice the lanes with
+            // 3/4 of the per-lane work, for launches bound by one wave's latency
+            const char* npe = std::getenv("NART_COL4_NP");
+            const bool np2 = npe && std::atoi(npe) == 2;
+            const uint64_t n2 = (uint64_t)nbk * g.tile_size * ((g.tile_size + 1) / 2);
+            if (sa.lut && np2)
+                hipLaunchKernelGGL((k_splat_col4<2, true>), dim3((uint32_t)((n2 + 255) / 256)), dim3(256), 0, st, sa);
+            else if (sa.lut)
                 hipLaunchKernelGGL((k_splat_col4<NART_SPLAT_NP, true>), dim3((uint32_t)((n4 + 255) / 256)), dim3(256), 0,
                                    st, sa);
             else
