@@ -119,6 +119,8 @@ struct RenderArgs {
     uint32_t* ghead = nullptr;
     // with ghead: the n-th group taken is gorder[n] (null: slot order)
     const uint32_t* gorder = nullptr;
+    // k_primary: packet traversal (path.h traverse_packet) instead of one ray per lane
+    uint32_t packet = 0;
 };
 #define RQ_PRIO_BIT 0x80000000u
 #define RQ_PAIR_BIT 0x40000000u
@@ -962,7 +964,11 @@ __global__ __launch_bounds__(256) void k_primary(DScene S, RenderArgs A, uint32_
         }
         float bt;
         uint32_t bg;
-        traverse<COUNT>(S, ray, lightTMax, false, bt, bg, sc, nullptr, blockDim.x, cnt, nullptr, 0);
+        if (A.packet)
+            traverse_packet<COUNT>(S, ray, lightTMax, bt, bg, reinterpret_cast<uint4*>(s_dyn) + (threadIdx.x >> 6) * A.stack_depth,
+                                   cnt);
+        else
+            traverse<COUNT>(S, ray, lightTMax, false, bt, bg, sc, nullptr, blockDim.x, cnt, nullptr, 0);
         return bg;
     };
     if (so.stride == 1u && (A.spp & 7u) == 0u && (so.first & 7u) == 0u) {

@@ -329,6 +329,131 @@ ND bool traverse(const DScene& S, const Ray& r, float tmax, bool ANY, float& bes
     return bestG != NO_HIT;
 }
 
+// Packet traversal of a wave's coherent closest-hit queries (k_primary: the camera rays of a 16x4
+// pixel block at one sample index).  The wave walks one node at a time (node index, lane mask and
+// stack wave-uniform: the node and triangle records are read once per wave, not once per lane);
+// each lane in the node's mask tests the node's child boxes against its own ray and cull
+// distance, and a child is entered with the mask of the lanes that hit it, nearer child first by
+// majority.  A lane therefore tests exactly the leaves whose boxes its own ray reaches (a
+// different order than traverse(), possibly beyond its final cull distance): the closest hit
+// (minimum t, ties to the lowest scene index) is the same, t2 stays a lower bound of every other
+// hit and risky flags the same ties and NaNs or more -- so oc_resolve returns the reference octree's
+// answer as after traverse() (path.h trav_step, octree.h).  wstk: this wave's LDS stack, 16 B per
+// level.
+template <bool COUNT>
+ND void traverse_packet(const DScene& S, const Ray& r, float tmax, float& bestT, uint32_t& bestG, uint4* wstk,
+                        TraceCounters& cnt) {
+    bestT = tmax;
+    bestG = NO_HIT;
+    if (!S.geometry_visible) return;
+    Trav t;
+    trav_begin(S, r, tmax, false, t);
+    const uint32_t me = __lane_id();
+    int code = S.root;
+    uint64_t mask = __ballot(1);
+    int sp = 0;
+    const f3 op = permute(r.o, r.major);
+    for (;;) {
+        const bool in = (mask >> me) & 1ull;
+        bool pop = false;
+        if (code >= 0) {
+            const float4* np = reinterpret_cast<const float4*>(S.nodes + code);
+            const float4 a = np[0], b = np[1], c = np[2];
+            const int4 k = reinterpret_cast<const int4*>(np)[3];
+            const f3 inv = t.inv, oi = t.oi;
+            const float tx0 = fmaf(a.x, inv.x, oi.x), tx1 = fmaf(a.w, inv.x, oi.x);
+            const float ty0 = fmaf(a.y, inv.y, oi.y), ty1 = fmaf(b.x, inv.y, oi.y);
+            const float tz0 = fmaf(a.z, inv.z, oi.z), tz1 = fmaf(b.y, inv.z, oi.z);
+            const float n0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+            const float f0 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+            const float ux0 = fmaf(b.z, inv.x, oi.x), ux1 = fmaf(c.y, inv.x, oi.x);
+            const float uy0 = fmaf(b.w, inv.y, oi.y), uy1 = fmaf(c.z, inv.y, oi.y);
+            const float uz0 = fmaf(c.x, inv.z, oi.z), uz1 = fmaf(c.w, inv.z, oi.z);
+            const float n1 = fmaxf(fmaxf(fminf(ux0, ux1), fminf(uy0, uy1)), fminf(uz0, uz1));
+            const float f1 = fminf(fminf(fmaxf(ux0, ux1), fmaxf(uy0, uy1)), fmaxf(uz0, uz1));
+            const bool h0 = in && (n0 <= f0) && (f0 >= 0.f) && (n0 <= t.cullT);
+            const bool h1 = in && (n1 <= f1) && (f1 >= 0.f) && (n1 <= t.cullT);
+            if (COUNT && in) cnt.nodes++;
+            const uint64_t m0 = __ballot(h0), m1 = __ballot(h1);
+            const int c0 = __builtin_amdgcn_readfirstlane(k.x), c1 = __builtin_amdgcn_readfirstlane(k.y);
+            if (m0 && m1) {
+                const uint64_t p1 = __ballot(h0 && h1 && n1 < n0);
+                const bool one_first = 2 * __popcll(p1) > __popcll(m0 & m1);
+                const int fc = one_first ? c0 : c1;
+                const uint64_t fm = one_first ? m0 : m1;
+                wstk[sp] = make_uint4((uint32_t)fc, (uint32_t)fm, (uint32_t)(fm >> 32), 0u);
+                ++sp;
+                code = one_first ? c1 : c0;
+                mask = one_first ? m1 : m0;
+            } else if (m0) {
+                code = c0;
+                mask = m0;
+            } else if (m1) {
+                code = c1;
+                mask = m1;
+            } else {
+                pop = true;
+            }
+        } else {
+            const uint32_t lc = ~(uint32_t)code;
+            const uint32_t first = lc >> 5, count = (lc & 31u) + 1u;
+            const float4* tpp = S.tri_perm + 4 * ((size_t)r.major * S.num_leaf_tris + first);
+            if (in) {
+                // trav_step's leaf loop (closest hit), operation for operation
+                for (uint32_t i = 0; i < count; ++i) {
+                    if (COUNT) cnt.tris++;
+                    const float4 tb = tpp[4 * i], tc = tpp[4 * i + 1], dd = tpp[4 * i + 2], ta = tpp[4 * i + 3];
+                    f3 p0 = F3(tb.x - op.x, tb.y - op.y, tb.z - op.z);
+                    f3 p1 = F3(tb.w - op.x, tc.x - op.y, tc.y - op.z);
+                    f3 p2 = F3(tc.z - op.x, tc.w - op.y, dd.x - op.z);
+                    p0.x += p0.z * r.Sx;
+                    p0.y += p0.z * r.Sy;
+                    p1.x += p1.z * r.Sx;
+                    p1.y += p1.z * r.Sy;
+                    p2.x += p2.z * r.Sx;
+                    p2.y += p2.z * r.Sy;
+                    const float e0 = (p1.x * p2.y) - (p1.y * p2.x);
+                    const float e1 = (p2.x * p0.y) - (p2.y * p0.x);
+                    const float e2 = (p0.x * p1.y) - (p0.y * p1.x);
+                    if (!edges_accept(e0, e1, e2)) continue;
+                    const f3 n = F3(ta.x, ta.y, ta.z);
+                    const float den = dot(r.d, n);
+                    const float tt = (ta.w - dot(r.o, n)) / den;
+                    if (tt != tt) t.risky = true;
+                    if (!(tt > 0.f) || !(tt < t.tmax)) continue;
+                    const uint32_t g = __float_as_uint(dd.y);
+                    const uint32_t info = __float_as_uint(dd.z) & (fabsf(den) >= dd.w ? 0xFFFFFFFFu : 0x7FFFFFFFu);
+                    if (tt < t.bestT) {
+                        t.t2 = t.bestT;
+                        t.bestT = tt;
+                        t.bestG = g;
+                        t.bestInfo = info;
+                        t.cullT = oc_cull(S, tt);
+                    } else {
+                        if (tt == t.bestT) {
+                            t.risky = true;
+                            t.bestInfo = g < t.bestG ? info : t.bestInfo;
+                            t.bestG = g < t.bestG ? g : t.bestG;
+                        }
+                        t.t2 = fminf(t.t2, tt);
+                    }
+                }
+            }
+            pop = true;
+        }
+        if (pop) {
+            if (sp == 0) break;
+            --sp;
+            const uint4 e = wstk[sp];
+            code = __builtin_amdgcn_readfirstlane((int)e.x);
+            mask = ((uint64_t)__builtin_amdgcn_readfirstlane(e.z) << 32) | (uint64_t)__builtin_amdgcn_readfirstlane(e.y);
+        }
+    }
+    bestT = t.bestT;
+    bestG = t.bestG;
+    oc_resolve<COUNT>(S, r, tmax, false, t.risky, t.bestInfo, fminf(t.t2, oc_cull(S, t.bestT)), bestT, bestG, cnt);
+}
+
 // ---------------------------------------------------------------- Intersection
 struct Isect {
     f3 p, gn, sn, dpds, dpdt;

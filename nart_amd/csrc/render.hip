@@ -629,8 +629,12 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     if (rq && primary && ctx->d_prim && a.cost == nullptr) {
         // (staging the top BVH nodes in LDS, as the path kernel does, measured slower here: a
         // wave's coherent rays read the same node, which the L1 broadcasts: 9.7 vs 8.2 ms at 64 spp)
+        // NART_PRIMARY_PACKET (read per call): 1 wave-packet traversal of the camera rays, 0 one ray per lane
+        RenderArgs pa = a;
+        const char* pp = std::getenv("NART_PRIMARY_PACKET");
+        pa.packet = pp ? (uint32_t)(std::atoi(pp) != 0) : 0u;
         hipLaunchKernelGGL((k_primary<COUNT, ENV>), dim3((a.n_slots + 255) / 256), dim3(256),
-                           (size_t)ctx->stack_depth * 256 * 8, st, ctx->scene, a, ctx->d_prim);
+                           (size_t)ctx->stack_depth * 256 * 8, st, ctx->scene, pa, ctx->d_prim);
         HIPCHK(hipGetLastError());
         if (ctx->events) {
             HIPCHK(hipEventRecord(ctx->ev[4], st));

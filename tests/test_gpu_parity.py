@@ -449,3 +449,40 @@ def test_c4_teapot_per_sample(gpu, c4_scene):
     g = nart_amd.HipRenderer(c4_scene).render_samples(p, 176, 96, 24, 16)
     r = oracle.Oracle(c4_scene).render_samples(p, 176, 96, 24, 16)
     assert _bits_equal(g, r), _report(g, r)
+
+
+@pytest.mark.parametrize("packet", ["1"], ids=["packet"])
+def test_primary_packet_traversal(gpu, glass_scene, cornell_scene, c4_scene, monkeypatch, packet):
+    """Camera rays traced as wave packets (NART_PRIMARY_PACKET=1, path.h traverse_packet): the
+    wave walks one node at a time with a lane mask, each lane testing its own ray.  Same closest
+    hit and octree answer as per-lane traversal: C1 frame, the C3 block with a d.z == 0 camera ray,
+    the C2 buckets whose octree answer differs from the true closest hit, a sample the octree
+    misses, and the C4 teapot."""
+    import torch
+    monkeypatch.setenv("NART_PRIMARY_PACKET", packet)
+    o = oracle.Oracle(glass_scene)
+    p = _params(glass_scene, 256, 256, 16)
+    g = nart_amd.HipRenderer(glass_scene).render(p)
+    r = o.render(p)
+    assert _bits_equal(g, r), _report(g, r)
+    p = _params(glass_scene, 1920, 1080, 256)
+    g = nart_amd.HipRenderer(glass_scene).render_samples(p, 1344, 128, 16, 16)
+    r = o.render_samples(p, 1344, 128, 16, 16)
+    assert _bits_equal(g, r), _report(g, r)
+    p = _params(cornell_scene, 1920, 1080, 64)
+    gm = nart_amd.session_geometry(p)
+    ids = np.array(C2_OCTREE_BUCKETS, np.uint32)
+    tiles = torch.zeros((len(ids), gm.tile_size * gm.tile_size, 5), dtype=torch.float32, device="cuda")
+    nart_amd.HipRenderer(cornell_scene).render_buckets_async(p, ids, tiles.data_ptr(),
+                                                             torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ref = oracle.Oracle(cornell_scene).render_buckets(p, ids)
+    got = tiles.cpu().numpy()
+    assert _bits_equal(got, ref), _report(got, ref)
+    gs = nart_amd.HipRenderer(cornell_scene).render_samples(p, 328, 232, 8, 8)
+    rs = oracle.Oracle(cornell_scene).render_samples(p, 328, 232, 8, 8)
+    assert _bits_equal(gs, rs), _report(gs, rs)
+    p = _params(c4_scene, 160, 90, 4)
+    g = nart_amd.HipRenderer(c4_scene).render(p)
+    r = oracle.Oracle(c4_scene).render(p)
+    assert _bits_equal(g, r), _report(g, r)
