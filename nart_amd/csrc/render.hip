@@ -629,10 +629,11 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     if (rq && primary && ctx->d_prim && a.cost == nullptr) {
         // (staging the top BVH nodes in LDS, as the path kernel does, measured slower here: a
         // wave's coherent rays read the same node, which the L1 broadcasts: 9.7 vs 8.2 ms at 64 spp)
-        // NART_PRIMARY_PACKET (read per call): 1 wave-packet traversal of the camera rays, 0 one ray per lane
+        // camera rays as wave packets (path.h traverse_packet; C3 -1.7 ms, C4 -31 ms per frame,
+        // profiles/r04_primary_packet_ab.log); NART_PRIMARY_PACKET=0 (read per call): one ray per lane
         RenderArgs pa = a;
         const char* pp = std::getenv("NART_PRIMARY_PACKET");
-        pa.packet = pp ? (uint32_t)(std::atoi(pp) != 0) : 0u;
+        pa.packet = pp ? (uint32_t)(std::atoi(pp) != 0) : 1u;
         hipLaunchKernelGGL((k_primary<COUNT, ENV>), dim3((a.n_slots + 255) / 256), dim3(256),
                            (size_t)ctx->stack_depth * 256 * 8, st, ctx->scene, pa, ctx->d_prim);
         HIPCHK(hipGetLastError());
@@ -1201,14 +1202,7 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
             else hipLaunchKernelGGL((k_splat_skew<3, 2>), dim3(nblk), dim3(256), lds, st, sa);
         } else if (sa.thr && sa.invB != 0.f && splat_mode >= 3)
         {
-            // NART_COL4_NP=2 (read per call, A/B): two tile pixels per lane -- twice the lanes with
-            // 3/4 of the per-lane work, for launches bound by one wave's latency
-            const char* npe = std::getenv("NART_COL4_NP");
-            const bool np2 = npe && std::atoi(npe) == 2;
-            const uint64_t n2 = (uint64_t)nbk * g.tile_size * ((g.tile_size + 1) / 2);
-            if (sa.lut && np2)
-                hipLaunchKernelGGL((k_splat_col4<2, true>), dim3((uint32_t)((n2 + 255) / 256)), dim3(256), 0, st, sa);
-            else if (sa.lut)
+            if (sa.lut)
                 hipLaunchKernelGGL((k_splat_col4<NART_SPLAT_NP, true>), dim3((uint32_t)((n4 + 255) / 256)), dim3(256), 0,
                                    st, sa);
             else

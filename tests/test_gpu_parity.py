@@ -451,11 +451,11 @@ def test_c4_teapot_per_sample(gpu, c4_scene):
     assert _bits_equal(g, r), _report(g, r)
 
 
-@pytest.mark.parametrize("packet", ["1"], ids=["packet"])
+@pytest.mark.parametrize("packet", ["1", "0"], ids=["packet", "per-lane"])
 def test_primary_packet_traversal(gpu, glass_scene, cornell_scene, c4_scene, monkeypatch, packet):
-    """Camera rays traced as wave packets (NART_PRIMARY_PACKET=1, path.h traverse_packet): the
-    wave walks one node at a time with a lane mask, each lane testing its own ray.  Same closest
-    hit and octree answer as per-lane traversal: C1 frame, the C3 block with a d.z == 0 camera ray,
+    """Camera rays traced as wave packets (the default, path.h traverse_packet: the wave walks one
+    node at a time with a lane mask, each lane testing its own ray) or one ray per lane
+    (NART_PRIMARY_PACKET=0).  Same closest hit and octree answer either way: C1 frame, the C3 block with a d.z == 0 camera ray,
     the C2 buckets whose octree answer differs from the true closest hit, a sample the octree
     misses, and the C4 teapot."""
     import torch
