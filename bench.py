@@ -290,7 +290,7 @@ def main():
     # moves is `traffic` (rocprofv3 2 x FETCH_SIZE + WRITE_SIZE per launch) -> measured_frac, and
     # what limits the kernel shows in lane_utilization (SQ_THREAD_CYCLES_VALU / 64
     # SQ_ACTIVE_INST_VALU: divergent lanes) and valu_busy.
-    roofline = {"bound": "latency", "ceiling": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                 "achieved_kind": "algorithmic bytes per launch (SURVEY.md 8(d) per-sample model x traced samples)",
                 "limiter": "latency/issue: dependent LDS/L2 loads in BVH traversal and divergent lanes "
