@@ -2266,12 +2266,17 @@ __global__ __launch_bounds__(256) void k_splat_skew(SplatArgs A) {
             d2[2 * k] = dd.x;
             d2[2 * k + 1] = dd.y;
         }
+        // the W weight-cell reads are issued together, before the per-row branches (a read inside
+        // each branch waited for its own LDS round trip: W dependent waits per sample); a row that
+        // is not hit reads a clamped, valid cell and discards it
+        float4 ev[W];
+#pragma unroll
+        for (int k = 0; k < W; ++k) ev[k] = s_lut[max(0, min((int)(__float_as_uint(d2[k]) >> 16) - lut_b0, lut_last))];
 #pragma unroll
         for (int k = 0; k < W; ++k) {
             const bool hit = xhit && loy < ys[k + 1] && ys[k] < hiy;
             if (hit) {
-                const int cell = max(0, min((int)(__float_as_uint(d2[k]) >> 16) - lut_b0, lut_last));
-                const float4 e = s_lut[cell];
+                const float4 e = ev[k];
                 const float w = d2[k] >= e.x ? e.z : e.y;
                 const nd_f2v w2 = nd_f2v{w, w};
                 cxy[k] += nd_f2v{L.x, L.y} * w2;

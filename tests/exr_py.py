@@ -6,7 +6,7 @@ Written from the published OpenEXR file layout (magic, attribute header, chlist,
 per-chunk {y, size, data}) and its ZIP codec (zlib, then the byte predictor and the two-half
 interleave); it shares no code with the product's reader (nart_amd/csrc/host/scene_host.cpp), so
 comparing the two checks the ingestion of the reference's textures instead of self-comparing.
-PIZ is not restated here (the product's PIZ decoder stays "parity unpinned").
+PIZ is restated separately (tests/exr_piz_py.py) and used here chunk by chunk.
 """
 import struct
 import zlib
@@ -86,16 +86,17 @@ def _unrle(data, raw_size):
     return res.tobytes()
 
 
-def read_rgba_halves(path):
-    """(H, W, 4) uint16 half bit patterns in R, G, B, A order, top row first."""
+def read_rgba_halves(path, max_rows=None):
+    """(H, W, 4) uint16 half bit patterns in R, G, B, A order, top row first.  max_rows: decode
+    only the chunks that start above that row (the rest stays zero; PIZ in pure Python is slow)."""
     buf = open(path, "rb").read()
     hdr, pos = parse_header(buf)
     comp = hdr["compression"]
-    if comp not in (NONE, RLE, ZIPS, ZIP):
+    if comp not in (NONE, RLE, ZIPS, ZIP, PIZ):
         raise NotImplementedError("compression %d" % comp)
     xmin, ymin, xmax, ymax = hdr["window"]
     w, h = xmax - xmin + 1, ymax - ymin + 1
-    lines = 16 if comp == ZIP else 1
+    lines = {ZIP: 16, PIZ: 32}.get(comp, 1)
     nchunks = (h + lines - 1) // lines
     offsets = struct.unpack_from("<%dQ" % nchunks, buf, pos)
     chans = sorted(hdr["channels"], key=lambda c: c[0])
@@ -106,10 +107,16 @@ def read_rgba_halves(path):
         y, n = struct.unpack_from("<ii", buf, off)
         data = buf[off + 8:off + 8 + n]
         y0 = y - ymin
+        if max_rows is not None and y0 >= max_rows:
+            continue
         nl = min(lines, h - y0)
         raw = nl * w * sum(size[c[1]] for c in chans)
         if n < raw:
-            data = _unzip(data, raw) if comp in (ZIPS, ZIP) else (_unrle(data, raw) if comp == RLE else data)
+            if comp == PIZ:
+                from exr_piz_py import piz_chunk
+                data = piz_chunk(data, [c[1] for c in chans], w, nl)
+            else:
+                data = _unzip(data, raw) if comp in (ZIPS, ZIP) else (_unrle(data, raw) if comp == RLE else data)
         assert len(data) == raw
         q = 0
         for ln in range(nl):

@@ -209,8 +209,9 @@ def test_piz_textures_decode(built, rel, shape):
     """PIZ (wavelet + Huffman) textures the reference ships (HALF BGR, HALF Y, FLOAT Y): every
     chunk's Huffman stream must decode to exactly the chunk's sample count (the decoder rejects
     anything else), values are finite, in the texture's [0, 1] range and spatially smooth (a
-    wrong wavelet or LUT step yields noise).  No PIZ encoder or OpenEXR is available here, so
-    the texel values themselves are unpinned."""
+    wrong wavelet or LUT step yields noise).  No PIZ encoder or OpenEXR is available here; the texel
+    values are checked against an independent restatement of the codec in
+    tests/test_ingestion_independent.py::test_piz_textures_independently."""
     import numpy as np
     import nart_amd
     a = nart_amd.read_exr(os.path.join(REF, "input", "textures", rel))

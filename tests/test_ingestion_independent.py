@@ -132,3 +132,26 @@ def test_writer_output_decodes_independently(built, tmp_path, compression):
     with np.errstate(over="ignore"):  # values above 65504 round to inf, as Imath does
         want = nart_amd.finalize(p, img).astype(np.float16).view(np.uint16)
     assert np.array_equal(halves, want)
+
+
+REF_TEX = "/root/reference/input/textures"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_TEX), reason="reference checkout not present")
+@pytest.mark.parametrize("rel,rows", [("glassIceWater/iceCube_normal.exr", 512),
+                                      ("glassIceWater/iceCube_roughness.exr", 512),
+                                      ("glassIceWater/glass_roughness.exr", 64),
+                                      ("cameraLens/lens_roughness.exr", 64)])
+def test_piz_textures_independently(built, rel, rows):
+    """The reference's PIZ textures (texturepattern.cpp:111-128 through Imf::RgbaInputFile: HALF
+    BGR, HALF Y, FLOAT Y -> halves) decoded by the product's reader (host/exr_piz.cpp) and by the
+    test-side PIZ restatement (tests/exr_piz_py.py: canonical Huffman by code length, numpy
+    wavelet levels, reverse LUT) must agree half for half -- the whole 512^2 textures, the first
+    PIZ chunks of the 4096^2 ones (pure Python is slow)."""
+    import nart_amd
+    path = os.path.join(REF_TEX, rel)
+    mine, hdr = exr_py.read_rgba_halves(path, max_rows=rows)
+    assert hdr["compression"] == exr_py.PIZ
+    prod = nart_amd.read_exr(path).astype(np.float16).view(np.uint16)
+    assert prod.shape == mine.shape
+    assert np.array_equal(prod[:rows], mine[:rows]), int((prod[:rows] != mine[:rows]).sum())
