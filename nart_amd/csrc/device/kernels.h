@@ -1974,6 +1974,14 @@ __global__ __launch_bounds__(256) void k_splat(SplatArgs A) {
 // (source pixel raster, sample) order.  Per-sample work (position, bucket-edge tests, the
 // column test and x distance) is shared.  (Four horizontal pixels per lane measured slower:
 // lanes then read source pixels four apart and the L1 misses rose by a third.)
+// splat_lut cell of d2: clamp((bits(d2) >> 16) - b0, 0, last), the clamp as one v_med3_i32
+// (the compiler forms it only for constant bounds)
+ND int lut_cell(float d2, int b0, int last) {
+    const int c = (int)(__float_as_uint(d2) >> 16) - b0;
+    int r;
+    asm("v_med3_i32 %0, %1, 0, %2" : "=v"(r) : "v"(c), "s"(last));
+    return r;
+}
 typedef float nd_f2v __attribute__((ext_vector_type(2)));  // packed-math pairs (v_pk_mul/add_f32)
 template <int NP, bool LUT>
 __global__ __launch_bounds__(256) void k_splat_col4(SplatArgs A) {
@@ -2266,22 +2274,38 @@ __global__ __launch_bounds__(256) void k_splat_skew(SplatArgs A) {
             d2[2 * k] = dd.x;
             d2[2 * k + 1] = dd.y;
         }
-        // the W weight-cell reads are issued together, before the per-row branches (a read inside
+        // the W weight-cell reads are issued together, before any per-row branch (a read inside
         // each branch waited for its own LDS round trip: W dependent waits per sample); a row that
         // is not hit reads a clamped, valid cell and discards it
         float4 ev[W];
 #pragma unroll
-        for (int k = 0; k < W; ++k) ev[k] = s_lut[max(0, min((int)(__float_as_uint(d2[k]) >> 16) - lut_b0, lut_last))];
+        for (int k = 0; k < W; ++k) ev[k] = s_lut[lut_cell(d2[k], lut_b0, lut_last)];
+        // Row k is hit iff xhit && loy < ys_{k+1} && ys_k < hiy.  Both row tests are monotone in k
+        // (ys_k = yb + k exactly), so every row is hit iff row 0 passes the first and row W-1 the
+        // second -- all but never fails (a sample exactly on a pixel edge): the rows then accumulate
+        // without per-row branches (4-5 scalar exec-mask instructions and two compares per row).
+        if (xhit && loy < ys[1] && ys[W - 1] < hiy) {
 #pragma unroll
-        for (int k = 0; k < W; ++k) {
-            const bool hit = xhit && loy < ys[k + 1] && ys[k] < hiy;
-            if (hit) {
+            for (int k = 0; k < W; ++k) {
                 const float4 e = ev[k];
                 const float w = d2[k] >= e.x ? e.z : e.y;
                 const nd_f2v w2 = nd_f2v{w, w};
                 cxy[k] += nd_f2v{L.x, L.y} * w2;
                 czw[k] += nd_f2v{L.z, L.w} * w2;
                 cws[k] += w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < W; ++k) {
+                const bool hit = xhit && loy < ys[k + 1] && ys[k] < hiy;
+                if (hit) {
+                    const float4 e = ev[k];
+                    const float w = d2[k] >= e.x ? e.z : e.y;
+                    const nd_f2v w2 = nd_f2v{w, w};
+                    cxy[k] += nd_f2v{L.x, L.y} * w2;
+                    czw[k] += nd_f2v{L.z, L.w} * w2;
+                    cws[k] += w;
+                }
             }
         }
     };
