@@ -189,9 +189,13 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
         } else
 #endif
         if (t.code < nl) {
-#if defined(NART_NODE_DS) && defined(__HIP_DEVICE_COMPILE__)
-            // explicit LDS address space: ds_read_b128, not a flat load through the generic aperture
-            // (opt-in: C3 full frame 577 vs 570 ms with the flat load)
+#if !defined(NART_NODE_FLAT) && defined(__HIP_DEVICE_COMPILE__)
+            // explicit LDS address space: ds_read_b128, not a flat load through the generic aperture.
+            // A flat load counts against both the vector-memory and the LDS counters, and the
+            // compiler serialised the node's four flat loads behind waits for earlier triangle
+            // loads; the LDS loads issue together.  k_render_rq, C3: 346.3 -> 336.5 ms per frame,
+            // 1/8 shard 85.9 -> 81.9 ms (profiles/r04_node_ds_ab.log; round 1's k_render measured
+            // 577 vs 570 ms the other way).  -DNART_NODE_FLAT restores the flat load.
             typedef float v4f __attribute__((ext_vector_type(4)));
             typedef const __attribute__((address_space(3))) v4f lds_v4f;
             lds_v4f* np = (lds_v4f*)lnodes + 4 * t.code;

@@ -62,9 +62,22 @@ NHD float dg_lookup2(const DMedium& m, f3 p) {
 struct MajIter {  // RayMajorantIterator (media.cpp:138-255) for a width-1 grid
     float tCurrent, tMax;
     uint32_t idx;
-    f3 next, cross;
+    f3 next;
+    // The grid direction, not the crossing distances: crossDistance_i = |((1 / gD_i) * 1) * bs_i|
+    // (inf for gD_i == 0) is only ever read through nextCrossing_i after Next() stores it there,
+    // and a ray in a one-cell grid leaves the medium at that first crossing, so the reciprocals
+    // are formed when a later Next() reads the stored entry (cross_at), not per ray: three
+    // correctly rounded divisions fewer per scattering event, the same values when needed.
+    f3 gD;
+    uint32_t pend;     // 1 + the axis whose next entry holds a not yet formed crossDistance, or 0
     uint32_t stepPos;  // bit i: step[i] > 0 (only the sign of the step is ever used)
 };
+
+// crossDistance_i of the iterator constructor (media.cpp:172-177)
+NHD float cross_at(const DMedium& m, const MajIter& it, int i) {
+    const float g = comp(it.gD, i), bsi = m.bmax[i] - m.bmin[i];
+    return g == 0.f ? __builtin_inff() : gabs(((1.f / g) * 1.f) * bsi);
+}
 
 // Medium::SampleRay (media.cpp:281-324) + the iterator constructor.
 ND bool medium_sample_ray(const DMedium& m, f3 o, f3 d, MajIter& it) {
@@ -102,11 +115,8 @@ ND bool medium_sample_ray(const DMedium& m, f3 o, f3 d, MajIter& it) {
     pX = muls(pX, 1.f);
     f3 gD = normalize(sub(pX, pE));
     if (pX.x == pE.x && pX.y == pE.y && pX.z == pE.z) gD = F3(1.f, 0.f, 0.f);
-    f3 cd = F3(gabs(((1.f / gD.x) * 1.f) * bs.x), gabs(((1.f / gD.y) * 1.f) * bs.y), gabs(((1.f / gD.z) * 1.f) * bs.z));
-    if (gD.x == 0.f) cd.x = __builtin_inff();
-    if (gD.y == 0.f) cd.y = __builtin_inff();
-    if (gD.z == 0.f) cd.z = __builtin_inff();
-    it.cross = cd;
+    it.gD = gD;  // crossDistance: cross_at, when Next() needs it
+    it.pend = 0;
     float t3[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -122,6 +132,14 @@ ND bool medium_sample_ray(const DMedium& m, f3 o, f3 d, MajIter& it) {
 
 ND bool maj_next(const DMedium& m, MajIter& it, float& sigma, float& t0, float& t1, uint32_t* used = nullptr) {  // media.cpp:214-255
     if (it.tCurrent + 0.0001f > it.tMax) return false;
+    if (it.pend) {  // the crossDistance the previous call stored in nextCrossing
+        const int a = (int)it.pend - 1;
+        const float c = cross_at(m, it, a);
+        it.next.x = a == 0 ? c : it.next.x;
+        it.next.y = a == 1 ? c : it.next.y;
+        it.next.z = a == 2 ? c : it.next.z;
+        it.pend = 0;
+    }
     uint32_t choice = 0;
     if (it.next.x < it.next.y) choice += 4;
     if (it.next.x < it.next.z) choice += 2;
@@ -138,10 +156,11 @@ ND bool maj_next(const DMedium& m, MajIter& it, float& sigma, float& t0, float& 
     if (used) *used = it.idx;
     t0 = it.tCurrent;
     t1 = it.tCurrent + dt;
-    const float nx = it.next.x - dt, ny = it.next.y - dt, nz = it.next.z - dt;
-    it.next.x = index == 0 ? it.cross.x : nx;
-    it.next.y = index == 1 ? it.cross.y : ny;
-    it.next.z = index == 2 ? it.cross.z : nz;
+    // nextCrossing -= dt; nextCrossing[index] = crossDistance[index] (formed by the next call)
+    it.next.x -= dt;
+    it.next.y -= dt;
+    it.next.z -= dt;
+    it.pend = (uint32_t)index + 1u;
     it.idx += (it.stepPos >> index) & 1u;
     it.tCurrent += dt;
     return true;
