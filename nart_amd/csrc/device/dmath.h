@@ -117,37 +117,36 @@ NHD double reduce_fast(double x, const SinCosT* p, int* np) {
     *np = n;
     return x - n * p->hpi;
 }
-// Valid for |y| < 120 (the reference only evaluates angles in [0, 2*pi]); larger inputs
-// would need glibc's reduce_large, which the render path never reaches.
-NHD float glibc_sinf(float y) {
-    double x = y;
-    SinCosT t0 = sincos_table(0);
-    const float pio4f = (float)0x1.921FB54442D18p-1;
-    if (abstop12(y) < abstop12(pio4f)) {
-        double s = x * x;
-        if (abstop12(y) < abstop12(0x1p-12f)) return y;
-        return sinf_poly(x, s, &t0, 0);
-    }
+// sinf and cosf of one argument (glibc's sinf / cosf / sincosf share this reduction), without
+// branches: a wave whose lanes fall on both sides of glibc's |y| < pi/4 test used to run both
+// paths.  For 2^-12 <= |y| < 0.75 (abstop12(y) < abstop12(pi/4)) glibc evaluates the polynomials
+// on y itself, which is exactly the reduced path with n = 0 (x - 0 * pi/2 = x, sign +1, table
+// 0); below 2^-12 it returns y and 1.  The cosine polynomial of table 1 is table 0's with every
+// coefficient negated, i.e. exactly the negated value, so both polynomials are evaluated once
+// and assigned by the parity of n.  Valid for |y| < 120 (the reference only evaluates angles in
+// [0, 2*pi]); larger inputs would need glibc's reduce_large, which the render path never reaches.
+NHD void glibc_sincosf(float y, float& sn, float& cs) {
+    const SinCosT t0 = sincos_table(0);
     int n;
-    x = reduce_fast(x, &t0, &n);
-    double s = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;  // t0.sign[n & 3]
-    SinCosT t = sincos_table((n & 2) ? 1 : 0);
-    return sinf_poly(x * s, x * x, &t, n);
+    const double x = reduce_fast((double)y, &t0, &n);
+    const double sg = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;  // t0.sign[n & 3]
+    const double x2 = x * x;
+    const float ps = sinf_poly(x * sg, x2, &t0, 0);  // sine polynomial (either table)
+    float pc = sinf_poly(x * sg, x2, &t0, 1);        // cosine polynomial, table 0
+    pc = (n & 2) ? -pc : pc;                          // table 1
+    const bool tiny = abstop12(y) < abstop12(0x1p-12f);
+    sn = tiny ? y : ((n & 1) ? pc : ps);
+    cs = tiny ? 1.0f : ((n & 1) ? ps : pc);
+}
+NHD float glibc_sinf(float y) {
+    float s, c;
+    glibc_sincosf(y, s, c);
+    return s;
 }
 NHD float glibc_cosf(float y) {
-    double x = y;
-    SinCosT t0 = sincos_table(0);
-    const float pio4f = (float)0x1.921FB54442D18p-1;
-    if (abstop12(y) < abstop12(pio4f)) {
-        double x2 = x * x;
-        if (abstop12(y) < abstop12(0x1p-12f)) return 1.0f;
-        return sinf_poly(x, x2, &t0, 1);
-    }
-    int n;
-    x = reduce_fast(x, &t0, &n);
-    double s = ((n & 3) == 1 || (n & 3) == 2) ? -1.0 : 1.0;  // t0.sign[n & 3]
-    SinCosT t = sincos_table((n & 2) ? 1 : 0);
-    return sinf_poly(x * s, x * x, &t, n ^ 1);
+    float s, c;
+    glibc_sincosf(y, s, c);
+    return c;
 }
 
 // ---------------------------------------------------------------- RNG (rng.h:8-59)
@@ -174,32 +173,27 @@ NHD float acosf_rpoly(float z) {
     float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
     return p / q;
 }
+// The three argument ranges of the main path (|x| < 0.5, x < -0.5, x > 0.5) share one
+// polynomial-quotient evaluation on the range's z, one sqrt and one division, selected per lane
+// instead of branched (a wave holding all three ranges ran three quotients, two sqrts and four
+// divisions); each lane's result is its range's expression, operation for operation.
 NHD float glibc_acosf(float x) {
     const float pi = fbits(0x40490fdau), pio2_hi = fbits(0x3fc90fdau), pio2_lo = fbits(0x33a22168u);
     const int32_t hx = (int32_t)ubits(x);
     const int32_t ix = hx & 0x7fffffff;
     if (ix == 0x3f800000) return hx > 0 ? 0.0f : pi + 2.0f * pio2_lo;
     if (ix > 0x3f800000) return (x - x) / (x - x);
-    if (ix < 0x3f000000) {  // |x| < 0.5
-        if (ix <= 0x32800000) return pio2_hi + pio2_lo;
-        float z = x * x;
-        float r = acosf_rpoly(z);
-        return pio2_hi - (x - (pio2_lo - x * r));
-    }
-    if (hx < 0) {  // x < -0.5
-        float z = (1.0f + x) * 0.5f;
-        float r = acosf_rpoly(z);
-        float s = sqrtf(z);
-        float w = r * s - pio2_lo;
-        return pi - 2.0f * (s + w);
-    }
-    float z = (1.0f - x) * 0.5f;  // x > 0.5
-    float s = sqrtf(z);
-    float df = fbits(ubits(s) & 0xfffff000u);
-    float c = (z - df * df) / (s + df);
-    float r = acosf_rpoly(z);
-    float w = r * s + c;
-    return 2.0f * (df + w);
+    if (ix <= 0x32800000) return pio2_hi + pio2_lo;  // |x| < 2^-26 (inside |x| < 0.5)
+    const bool mid = ix < 0x3f000000, neg = hx < 0;   // |x| < 0.5; else x < -0.5 / x > 0.5
+    const float z = mid ? x * x : (neg ? (1.0f + x) * 0.5f : (1.0f - x) * 0.5f);
+    const float r = acosf_rpoly(z);
+    const float s = sqrtf(z);
+    const float df = fbits(ubits(s) & 0xfffff000u);
+    const float c = (z - df * df) / (s + df);
+    const float a_mid = pio2_hi - (x - (pio2_lo - x * r));
+    const float a_neg = pi - 2.0f * (s + (r * s - pio2_lo));
+    const float a_pos = 2.0f * (df + (r * s + c));
+    return mid ? a_mid : (neg ? a_neg : a_pos);
 }
 
 NHD float glibc_atanf(float x) {
@@ -211,43 +205,28 @@ NHD float glibc_atanf(float x) {
                 aT9 = fbits(0xbd15a221u), aT10 = fbits(0x3c8569d7u);
     const int32_t hx = (int32_t)ubits(x);
     const int32_t ix = hx & 0x7fffffff;
-    int id;
     if (ix >= 0x4c000000) {  // |x| >= 2^25
         if (ix > 0x7f800000) return x + x;
         return hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
     }
-    if (ix < 0x3ee00000) {  // |x| < 0.4375
-        if (ix < 0x31000000) return x;  // |x| < 2^-29
-        id = -1;
-    } else {
-        x = fabsf(x);
-        if (ix < 0x3f980000) {      // |x| < 1.1875
-            if (ix < 0x3f300000) {  // 7/16 <= |x| < 11/16
-                id = 0;
-                x = (2.0f * x - 1.0f) / (2.0f + x);
-            } else {
-                id = 1;
-                x = (x - 1.0f) / (x + 1.0f);
-            }
-        } else {
-            if (ix < 0x401c0000) {  // |x| < 2.4375
-                id = 2;
-                x = (x - 1.5f) / (1.0f + 1.5f * x);
-            } else {
-                id = 3;
-                x = -1.0f / x;
-            }
-        }
-    }
+    if (ix < 0x31000000) return x;  // |x| < 2^-29
+    // the argument reduction's four quotients as one division of selected operands (per lane
+    // the same numerator and denominator expressions; lanes of the |x| < 0.4375 range discard it)
+    const int id = ix < 0x3ee00000 ? -1 : ix < 0x3f300000 ? 0 : ix < 0x3f980000 ? 1 : ix < 0x401c0000 ? 2 : 3;
+    const float ax = fabsf(x);
+    const float num = id == 0 ? 2.0f * ax - 1.0f : id == 1 ? ax - 1.0f : id == 2 ? ax - 1.5f : -1.0f;
+    const float den = id == 0 ? 2.0f + ax : id == 1 ? ax + 1.0f : id == 2 ? 1.0f + 1.5f * ax : ax;
+    const float q = num / den;
+    x = id < 0 ? x : q;
     float z = x * x;
     float w = z * z;
     float s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
     float s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
-    if (id < 0) return x - x * (s1 + s2);
-    float hi = id == 0 ? atanhi[0] : id == 1 ? atanhi[1] : id == 2 ? atanhi[2] : atanhi[3];
-    float lo = id == 0 ? atanlo[0] : id == 1 ? atanlo[1] : id == 2 ? atanlo[2] : atanlo[3];
+    const float small = x - x * (s1 + s2);
+    const float hi = id == 0 ? atanhi[0] : id == 1 ? atanhi[1] : id == 2 ? atanhi[2] : atanhi[3];
+    const float lo = id == 0 ? atanlo[0] : id == 1 ? atanlo[1] : id == 2 ? atanlo[2] : atanlo[3];
     z = hi - ((x * (s1 + s2) - lo) - x);
-    return hx < 0 ? -z : z;
+    return id < 0 ? small : (hx < 0 ? -z : z);
 }
 
 NHD float glibc_atan2f(float y, float x) {
@@ -358,13 +337,15 @@ ND uint32_t rng_int(uint32_t& y, uint32_t max) {
 ND f2 uniform_sample_disk(f2 s) {  // sampling.cpp:5-16
     float r = sqrtf(s.x);
     float theta = s.y * ND_TWO_PI;
-    float c = glibc_cosf(theta), sn = glibc_sinf(theta);
+    float c, sn;
+    glibc_sincosf(theta, sn, c);
     return F2(r * c, r * sn);
 }
 ND f2 uniform_sample_ring(f2 s, float& pdf, float inner) {  // sampling.cpp:18-31
     float r = sqrtf(gmix(inner, 1.f, s.x));
     float theta = s.y * ND_TWO_PI;
-    float c = glibc_cosf(theta), sn = glibc_sinf(theta);
+    float c, sn;
+    glibc_sincosf(theta, sn, c);
     pdf = 1.f / (ND_PI * (1.f - inner));
     return F2(r * c, r * sn);
 }

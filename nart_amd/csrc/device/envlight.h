@@ -76,8 +76,10 @@ ND f3 light_sample_li(const DScene& S, const DLight& L, f3 p, f3& wi, f2 sample,
         phi += ND_PI;
         if (phi > ND_TWO_PI) phi -= ND_TWO_PI;
         if (phi < 0.f) phi += ND_TWO_PI;
-        const float st = glibc_sinf(theta);
-        wi = F3(glibc_cosf(phi) * st, glibc_sinf(phi) * st, glibc_cosf(theta));
+        float st, ct, sp, cp;
+        glibc_sincosf(theta, st, ct);
+        glibc_sincosf(phi, sp, cp);
+        wi = F3(cp * st, sp * st, ct);
         pdf *= ND_ONE_OVER_PI * 0.25f / gabs(st);
         tMax = ENV_TMAX;
         return Lv;

@@ -14,8 +14,9 @@ namespace nd {
 ND f3 uniform_sample_sphere(f2 smp) {  // sampling.cpp:33-45 (pdf unused by the caller)
     const float theta = glibc_acosf(1.f - (2.f * smp.x));
     const float phi = smp.y * ND_TWO_PI;
-    const float cosTheta = glibc_cosf(theta), sinTheta = glibc_sinf(theta);
-    const float cosPhi = glibc_cosf(phi), sinPhi = glibc_sinf(phi);
+    float cosTheta, sinTheta, cosPhi, sinPhi;
+    glibc_sincosf(theta, sinTheta, cosTheta);
+    glibc_sincosf(phi, sinPhi, cosPhi);
     return F3(sinTheta * cosPhi, sinTheta * sinPhi, cosTheta);
 }
 

@@ -1,7 +1,9 @@
 """The device libm port (dmath.h: glibc 2.35 sinf/cosf algorithm in double precision) against
 the host glibc the reference links (glm::sin / glm::cos -> sinf / cosf).  Host build of the
 same source; the GPU build is checked in test_gpu_parity.py.  An exhaustive sweep (stride 1)
-over [-2*pi, 2*pi] found 0 mismatches in 2.17e9 values; CI runs a strided sweep."""
+over [-2*pi, 2*pi] found 0 mismatches in 2.17e9 values; CI runs a strided sweep.  Both sweeps
+were repeated on the branch-free forms (round 4: glibc_sincosf, and acosf / atanf with one
+quotient evaluation per lane): 0 mismatches."""
 import os
 import shutil
 import subprocess
