@@ -232,6 +232,21 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
         float f1 = fminf(fminf(fmaxf(ux0, ux1), fmaxf(uy0, uy1)), fmaxf(uz0, uz1));
         bool h0 = (n0 <= f0) && (f0 >= 0.f) && (n0 <= t.cullT);
         bool h1 = (n1 <= f1) && (f1 >= 0.f) && (n1 <= t.cullT);
+#if !defined(NART_TRAV_BRANCH) && !defined(NART_ORDER)
+        {
+            // the child choice as selects: the far child is written to the free slot at sp on
+            // every step and kept (sp + 1) only when both children are entered (sp <= max_stack <
+            // stack_depth, so the write stays inside the lane's stack); the same entries, order
+            // and codes as the branches below (-DNART_TRAV_BRANCH), with fewer exec-mask
+            // instructions per node: C3 321 -> 316 ms, 1/8 shard 81 -> 77 ms (profiles/r04t_*)
+            const bool both = h0 && h1, swap = n1 < n0;
+            stk_push(sc, st, stride, t.sp, swap ? k.x : k.y, swap ? n0 : n1);
+            t.sp += both ? 1 : 0;
+            t.code = both ? (swap ? k.y : k.x) : (h0 ? k.x : k.y);
+            if (!h0 && !h1 && !trav_pop(t, sc, st, stride)) return true;
+            continue;
+        }
+#endif
         if (h0 && h1) {
 #if defined(NART_ORDER) && NART_ORDER == 1
             // entry distances clamped to the origin; ties (both boxes hold the origin) by exit
@@ -666,46 +681,47 @@ ND f3 bxdf_f_pdf(const BxDF& b, f3 wo, f3 wi, bool uap, float eta_outer, float& 
         return muls(b.rho, ND_ONE_OVER_PI);
     }
     if (b.type == B_DIEL) {  // dielectricbrdf.cpp:31-80 (f), 187-225 (Pdf)
+        // Reflection (wo.z * wi.z >= 0) and transmission evaluate the same chain -- half vector,
+        // D, the Smith terms, Fresnel -- on different inputs: the reflection half vector is
+        // normalize(wo + wi) = normalize(wo * 1 + wi * 1) (x * 1 is exact) and its Fresnel argument
+        // |dot(wh, wo)| = |dot(wo, wh)|.  A wave whose glass lanes both reflect and transmit ran
+        // the chain twice; here it runs once on per-lane selected inputs, and each division takes
+        // the numerator and denominator of the lane's own branch.  Every lane computes its
+        // branch's values with its branch's operations.
         const float alpha = uap ? b.ap : b.a0;
         float eta_o = eta_outer, eta_i = b.eta;
         const bool same = eta_o == eta_i;
         const float lo = lambda_(alpha, wo);
-        if (wo.z * wi.z >= 0.f) {
-            // reflection: f swaps the etas for wo.z < 0, Pdf does not need them
-            if (wo.z < 0.f) { float t = eta_o; eta_o = eta_i; eta_i = t; }
-            f3 wh = normalize(add(wo, wi));
-            if (wh.z < 0.f) wh = muls(wh, -1.f);
-            const float d = D_diel(alpha, wh);
-            if (!same) {
-                const float cosThetaH = gabs(gmin(dot(wo, wh), 1.f));
-                const float p = (d * gmin(dot(wo, wh), 1.f) * (1.f / (1.f + lo))) / wo.z;
-                pdf = gmax(0.f, p / (4.f * cosThetaH));
-            }
-            const float g = 1.f / (1.f + lo + lambda_(alpha, wi));
-            const float Fr = fresnel(eta_o, eta_i, gabs(dot(wh, wo)));
-            if (wo.z * wi.z == 0.f) return F3(0.f, 0.f, 0.f);
-            return divs(muls(muls(muls(b.rho, g), d), Fr), (4.f * wo.z * wi.z));
-        }
-        if (wo.z < 0.f) { float t = eta_o; eta_o = eta_i; eta_i = t; }
-        f3 wh = normalize(add(muls(wo, eta_o), muls(wi, eta_i)));
+        const bool refl = wo.z * wi.z >= 0.f;
+        if (wo.z < 0.f) { float t = eta_o; eta_o = eta_i; eta_i = t; }  // f swaps in both branches
+        const float ea = refl ? 1.f : eta_o, eb = refl ? 1.f : eta_i;
+        f3 wh = normalize(add(muls(wo, ea), muls(wi, eb)));
         if (wh.z < 0.f) wh = muls(wh, -1.f);
         const float d = D_diel(alpha, wh);
         const float wiDotWh = dot(wi, wh);
         const float woDotWh = dot(wo, wh);
         if (!same) {
-            const float p = (d * gmin(gabs(woDotWh), 1.f) * (1.f / (1.f + lo))) / gabs(wo.z);
+            // reflection: (d * min(wo.wh, 1) * G1) / wo.z, then max(0, p / (4 |min(wo.wh, 1)|));
+            // transmission: (d * min(|wo.wh|, 1) * G1) / |wo.z|, then p * (|wi.wh| eta_i^2) / denom^2
+            const float p = (d * gmin(refl ? woDotWh : gabs(woDotWh), 1.f) * (1.f / (1.f + lo))) /
+                            (refl ? wo.z : gabs(wo.z));
+            const float cosThetaH = gabs(gmin(woDotWh, 1.f));
             const float denom = (eta_i * wiDotWh + eta_o * woDotWh);
-            const float JDet = (fabsf(wiDotWh) * eta_i * eta_i) / (denom * denom);
-            pdf = p * JDet;
+            const float r = (refl ? p : fabsf(wiDotWh) * eta_i * eta_i) / (refl ? 4.f * cosThetaH : denom * denom);
+            pdf = refl ? gmax(0.f, r) : p * r;
         }
         const float Fr = fresnel(eta_o, eta_i, gabs(woDotWh));
-        if (Fr >= 1.f) return F3(0.f, 0.f, 0.f);
         const float g = 1.f / (1.f + lo + lambda_(alpha, wi));
+        // f: reflection rho_c * g * d * Fr / (4 wo.z wi.z) per channel; transmission
+        // (g d (1 - Fr) |wi.wh| |wo.wh| eta_o^2) / (x^2 |wo.z wi.z|) times tau_c
         const float num = g * d * (1.f - Fr) * gabs(wiDotWh) * gabs(woDotWh) * eta_o * eta_o;
         const float x = ((eta_i * wiDotWh) + (eta_o * woDotWh));
-        const float denom = x * x * gabs(wo.z * wi.z);
-        const float q = num / denom;
-        return mul(F3(q, q, q), b.tau);
+        const float den = refl ? (4.f * wo.z * wi.z) : x * x * gabs(wo.z * wi.z);
+        const float qx = (refl ? ((b.rho.x * g) * d) * Fr : num) / den;
+        const float qy = (refl ? ((b.rho.y * g) * d) * Fr : num) / den;
+        const float qz = (refl ? ((b.rho.z * g) * d) * Fr : num) / den;
+        if (refl ? wo.z * wi.z == 0.f : Fr >= 1.f) return F3(0.f, 0.f, 0.f);
+        return refl ? F3(qx, qy, qz) : mul(F3(qx, qx, qx), b.tau);
     }
     if (b.type == B_TS) {  // torrancesparrowbrdf.cpp:32-51 (f), 109-124 (Pdf)
         const float alpha = uap ? b.ap : b.a0;
@@ -795,33 +811,24 @@ ND f3 bxdf_sample_f(const BxDF& b, f3 wo, f3& wi, float s1, f2 sample, float& pd
         f3 wh = sample_wh(wo, alpha, sample, true);
         if (wo.z < 0.f) { float t = eta_o; eta_o = eta_i; eta_i = t; }
         float Fr = fresnel(eta_o, eta_i, gabs(dot(wh, wo)));
-        if (s1 < Fr) {
-            wi = normalize(reflect(wo, wh));
-            float pp;
-            const f3 fr = bxdf_f_pdf(b, wo, wi, uap, eta_outer, pp);
-            pdf = pp * Fr;
-            return fr;
-        }
+        // reflection (s1 < Fr), total internal reflection and refraction each end with
+        // bxdf_f_pdf of their wi: one evaluation on the lane's wi (each lane's wi and pdf factor
+        // are its branch's), not one per branch present in the wave
+        const bool rf = s1 < Fr;
         float cos_o = gmin(1.f, gmax(-1.f, dot(wo, wh)));
         float sin_o = sqrtf(1.f - (cos_o * cos_o));
         float sin_i = ((eta_o / eta_i) * sin_o);
-        if (sin_i >= 1.f) {
-            wi = normalize(reflect(wo, wh));
-            float pp;
-            const f3 fr = bxdf_f_pdf(b, wo, wi, uap, eta_outer, pp);
-            pdf = pp * (1.f - Fr);
-            return fr;
-        }
-        flags |= F_TRANSMISSIVE;
+        const bool tr = !rf && !(sin_i >= 1.f);
         f3 bb = muls(wh, cos_o);
         f3 a = sub(wo, bb);
         f3 c = muls(neg(a), (eta_o / eta_i));
         f3 d = muls(neg(wh), sqrtf(1.f - (sin_i * sin_i)));
         if (dot(wo, wh) < 0.f) d = muls(d, -1.f);
-        wi = normalize(add(c, d));
+        if (tr) flags |= F_TRANSMISSIVE;
+        wi = normalize(tr ? add(c, d) : reflect(wo, wh));
         float pp;
         const f3 fr = bxdf_f_pdf(b, wo, wi, uap, eta_outer, pp);
-        pdf = pp * (1.f - Fr);
+        pdf = pp * (rf ? Fr : (1.f - Fr));
         return fr;
     }
     // B_TS: torrancesparrowbrdf.cpp:53-105
