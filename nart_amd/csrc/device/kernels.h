@@ -769,7 +769,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
                 float bsmp = rng_float(rng);
                 uint32_t dflags = 0;
                 f3 wi;
-                f3 f = bsdf_sample_f(bsdf, wo, wi, bsmp, F2(sx, sy), sPdf, dflags, true, eta_outer, nullptr, nullptr);
+                f3 f = bsdf_sample_f<ENV>(bsdf, wo, wi, bsmp, F2(sx, sy), sPdf, dflags, true, eta_outer, nullptr, nullptr);
                 if (sPdf > 0.f) {
                     float flip = wi.z > 0.f ? 1.f : -1.f;
                     f3 wW = to_world(bsdf, wi);
@@ -824,7 +824,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
                 float bs2 = rng_float(rng);
                 float cpdf = 0.f, alpha_i = 0.f;
                 f3 wic;
-                f3 fc = bsdf_sample_f(bsdf, wo, wic, bs2, F2(a, b), cpdf, flags, false, eta_outer, &alpha_i,
+                f3 fc = bsdf_sample_f<ENV>(bsdf, wo, wic, bs2, F2(a, b), cpdf, flags, false, eta_outer, &alpha_i,
                                       &eta_sampled);
                 if (cpdf <= 0.f) {
                     cont = false;
@@ -1533,7 +1533,7 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                 float bsmp = draw();
                 uint32_t dflags = 0;
                 f3 wi;
-                f3 f = bsdf_sample_f(bsdf, wo, wi, bsmp, F2(sx, sy), sPdf, dflags, true, eta_outer, nullptr,
+                f3 f = bsdf_sample_f<ENV>(bsdf, wo, wi, bsmp, F2(sx, sy), sPdf, dflags, true, eta_outer, nullptr,
                                      nullptr);
                 if (sPdf > 0.f) {
                     float flip = wi.z > 0.f ? 1.f : -1.f;
@@ -1581,7 +1581,7 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                 float bs2 = draw();
                 float cpdf = 0.f, alpha_i = 0.f;
                 f3 wic;
-                f3 fc = bsdf_sample_f(bsdf, wo, wic, bs2, F2(a, b), cpdf, flags, false, eta_outer, &alpha_i,
+                f3 fc = bsdf_sample_f<ENV>(bsdf, wo, wic, bs2, F2(a, b), cpdf, flags, false, eta_outer, &alpha_i,
                                       &eta_sampled);
                 if (cpdf <= 0.f) {
                     cont = false;

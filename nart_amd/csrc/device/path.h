@@ -885,23 +885,75 @@ ND f3 bsdf_f_pdf(const BSDF& s, f3 wo, f3 wi, bool uap, float eta_outer, float& 
     pdf = p / (float)s.num;
     return f;
 }
+// SHARE_TS: the environment-light builds of the path kernels (C4: 3,332 -> 3,259 ms); the others
+// keep one evaluation per role (C3 measured 316 -> 322 ms with sharing, a register-allocation
+// effect in the 256-VGPR kernel, which has no plastic lobes to share; profiles/r04y_share_ts_ab.log)
+template <bool SHARE_TS = true>
 ND f3 bsdf_sample_f(const BSDF& s, f3 wo, f3& wi, float s1, f2 sample, float& pdf, uint32_t& flags, bool uap,
                     float eta_outer, float* alpha_i, float* eta_i) {
+    if (!SHARE_TS) {
+        uint32_t idx = f2u8(s1 * (float)s.num);
+        s1 = gfract(s1 * (float)s.num);
+        const BxDF& sel = s.b[idx ? 1 : 0];
+        f3 f = bxdf_sample_f(sel, wo, wi, s1, sample, pdf, flags, alpha_i, uap, eta_outer);
+        if (eta_i && (flags & F_TRANSMISSIVE)) *eta_i = bxdf_eta(sel);
+        if (!(flags & F_SPECULAR)) {
+            if (s.num > 1) {
+                const BxDF& o = s.b[idx ? 0 : 1];
+                if (!(o.flags & F_SPECULAR)) {
+                    float bp;
+                    const f3 fo = bxdf_f_pdf(o, wo, wi, uap, eta_outer, bp);
+                    if (bp > 0.f) {
+                        pdf += bp;
+                        f = add(f, fo);
+                    }
+                }
+            }
+            pdf /= (float)s.num;
+        }
+        return f;
+    }
     uint32_t idx = f2u8(s1 * (float)s.num);
     s1 = gfract(s1 * (float)s.num);
     const BxDF& sel = s.b[idx ? 1 : 0];
-    f3 f = bxdf_sample_f(sel, wo, wi, s1, sample, pdf, flags, alpha_i, uap, eta_outer);
+    const BxDF& o = s.b[idx ? 0 : 1];
+    // The GGX reflection lobe (B_TS) is evaluated at the sampled wi either as the sampled lobe
+    // (torrancesparrowbrdf.cpp:53-105 ends with Pdf and f) or as a plastic's other lobe
+    // (bxdf.cpp:87-106): a wave holding both kinds of lanes ran that evaluation twice.  Here the
+    // B_TS sampling step only draws wi, and one bxdf_f_pdf serves both roles, with the lane's own
+    // lobe and wi (the sums below take the same operands; + is commutative).
+    const bool ts_sel = sel.type == B_TS;
+    f3 f = F3(0.f, 0.f, 0.f);
+    if (ts_sel) {  // torrancesparrowbrdf.cpp:53-105 up to the direction
+        float alpha = uap ? sel.ap : sel.a0;
+        if (alpha_i) *alpha_i = alpha;
+        flags = F_SPECULAR;
+        if (alpha > 0.001f) flags = F_GLOSSY;
+        if (alpha >= 1.0f) flags = F_DIFFUSE;
+        f3 wh = sample_wh(wo, alpha, sample, false);
+        wi = normalize(reflect(wo, wh));
+    } else {
+        f = bxdf_sample_f(sel, wo, wi, s1, sample, pdf, flags, alpha_i, uap, eta_outer);
+    }
     if (eta_i && (flags & F_TRANSMISSIVE)) *eta_i = bxdf_eta(sel);
+    // (o is read only for two-lobe BSDFs: s.num > 1 is tested first)
+    const bool other = !(flags & F_SPECULAR) && s.num > 1 && !(o.flags & F_SPECULAR);
+    const bool other_ts = other && !ts_sel && o.type == B_TS;
+    float tp = 0.f;
+    f3 tf = F3(0.f, 0.f, 0.f);
+    if (ts_sel || other_ts) tf = bxdf_f_pdf(ts_sel ? sel : o, wo, wi, uap, eta_outer, tp);
+    if (ts_sel) {
+        f = tf;
+        pdf = tp;
+    }
     if (!(flags & F_SPECULAR)) {
-        if (s.num > 1) {
-            const BxDF& o = s.b[idx ? 0 : 1];
-            if (!(o.flags & F_SPECULAR)) {
-                float bp;
-                const f3 fo = bxdf_f_pdf(o, wo, wi, uap, eta_outer, bp);
-                if (bp > 0.f) {
-                    pdf += bp;
-                    f = add(f, fo);
-                }
+        if (other) {
+            float bp = tp;
+            f3 fo = tf;
+            if (!other_ts) fo = bxdf_f_pdf(o, wo, wi, uap, eta_outer, bp);
+            if (bp > 0.f) {
+                pdf += bp;
+                f = add(f, fo);
             }
         }
         pdf /= (float)s.num;
