@@ -16,10 +16,13 @@ ND float env_ptn_pdf(const DScene& S, const DLight& L, f2 st) {
 
 // Light::Li (disklight.cpp:12-23, ringlight.cpp:117-128, environmentlight.cpp:9-28).
 // ENV = false compiles the environment branch out (scenes without one): it costs registers.
+// theta_in: acosf(wi.z) already formed by the caller (k_render_volume_sm shares that evaluation
+// with its scattering phase), or NAN to form it here
 template <bool ENV = true>
-ND f3 light_li(const DScene& S, const DLight& L, f3 p, f3 wi, float* pdf, float& tMax) {
+ND f3 light_li(const DScene& S, const DLight& L, f3 p, f3 wi, float* pdf, float& tMax,
+               float theta_in = __builtin_nanf("")) {
     if (ENV && L.type == NART_LIGHT_ENVIRONMENT) {
-        const float theta = glibc_acosf(wi.z);
+        const float theta = theta_in == theta_in ? theta_in : glibc_acosf(wi.z);
         float phi = glibc_atan2f(wi.y, wi.x) + ND_PI;
         if (phi > ND_TWO_PI) phi -= ND_TWO_PI;
         if (phi < 0.f) phi += ND_TWO_PI;

@@ -334,6 +334,35 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
     MajIter it;
     for (;;) {
         bool finish = false;
+        // The scattering phase's UniformSampleSphere (volumeintegrator.cpp:44-47) and the escape
+        // phase's environment lookup (environmentlight.cpp:9-28) both begin with an acosf: one
+        // evaluation per lane per iteration serves the lane's phase.  The escape phase therefore
+        // runs at the top of the iteration after the one that chose it (and the lane starts its
+        // next sample in that same iteration, as before): each lane's operations and their order
+        // are unchanged.
+        const bool scat = ph == P_SCAT, esc = ph == P_ESC;
+        float sa = 0.f, sb = 0.f, theta = 0.f;
+        if (scat) {
+            sa = rng_float(rng);
+            sb = rng_float(rng);
+        }
+        if (scat || esc) theta = glibc_acosf(scat ? 1.f - (2.f * sa) : d.z);
+        if (esc) {
+            float lightTMax = __builtin_inff();
+            f3 Le = F3(0.f, 0.f, 0.f);
+            for (uint32_t j = 0; j < S.num_lights; ++j) {
+                float lt = __builtin_inff();
+                const f3 Li = light_li(S, S.lights[j], o, d, nullptr, lt, theta);
+                if (lt < lightTMax) {
+                    Le = Li;
+                    lightTMax = lt;
+                }
+            }
+            L = add(L, mul(Le, beta));
+            out[(size_t)s * so.stride] = make_float4(L.x, L.y, L.z, 1.f);
+            ++s;
+            ph = P_SAMPLE;
+        }
         if (ph == P_SAMPLE) {
             if (s >= A.spp) break;
             const float2 sm = smp[(size_t)s * so.stride];
@@ -344,10 +373,12 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
             bounce = 0;
             ph = P_RAY;
         }
-        if (ph == P_SCAT) {  // isotropic scattering direction (volumeintegrator.cpp:44-47)
-            const float a = rng_float(rng);
-            const float b = rng_float(rng);
-            d = uniform_sample_sphere(F2(a, b));
+        if (scat) {  // the rest of UniformSampleSphere (sampling.cpp:33-45)
+            const float phi = sb * ND_TWO_PI;
+            float cosTheta, sinTheta, cosPhi, sinPhi;
+            glibc_sincosf(theta, sinTheta, cosTheta);
+            glibc_sincosf(phi, sinPhi, cosPhi);
+            d = F3(sinTheta * cosPhi, sinTheta * sinPhi, cosTheta);
             ph = P_RAY;
         }
         if (ph == P_RAY) {  // top of VolumeIntegrator's bounce loop
@@ -399,14 +430,14 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
                     const f3 qn = m.bs_pow2 == 7u ? F3(q0.x * m.inv_bs[0], q0.y * m.inv_bs[1], q0.z * m.inv_bs[2])
                                                   : F3(q0.x / bs.x, q0.y / bs.y, q0.z / bs.z);
                     const float density = m.grid2 ? dg_lookup2(m, qn) : dg_lookup(m, dens, qn);
-                    const float sa = m.sigma_a * density, ss = m.sigma_s * density;
+                    const float ca = m.sigma_a * density, cs = m.sigma_s * density;
                     float pAbsorb, pScatter;
                     if (sp2) {
-                        pAbsorb = sa * isig;
-                        pScatter = ss * isig;
+                        pAbsorb = ca * isig;
+                        pScatter = cs * isig;
                     } else {
-                        pAbsorb = sa / sigma;
-                        pScatter = ss / sigma;
+                        pAbsorb = ca / sigma;
+                        pScatter = cs / sigma;
                     }
                     if (uMode < pAbsorb) {
                         L = add(L, mul(muls(F3(m.Le[0], m.Le[1], m.Le[2]), density), beta));
@@ -424,20 +455,6 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
                     }
                 }
             }
-        }
-        if (ph == P_ESC) {
-            float lightTMax = __builtin_inff();
-            f3 Le = F3(0.f, 0.f, 0.f);
-            for (uint32_t j = 0; j < S.num_lights; ++j) {
-                float lt = __builtin_inff();
-                const f3 Li = light_li(S, S.lights[j], o, d, nullptr, lt);
-                if (lt < lightTMax) {
-                    Le = Li;
-                    lightTMax = lt;
-                }
-            }
-            L = add(L, mul(Le, beta));
-            finish = true;
         }
         if (finish) {
             out[(size_t)s * so.stride] = make_float4(L.x, L.y, L.z, 1.f);
