@@ -151,6 +151,76 @@ def kernel_ratios(prof, samples, tiles_bytes):
     return out or None
 
 
+def workload_name(cfg, a, W, H, SPP):
+    if not a.size:
+        return cfg["workload"]
+    return "%s, resized to %dx%d %dspp (rehearsal, not the bench workload)" % (cfg["workload"], W, H, SPP)
+
+
+def one_process_main(a, cfg, W, H, SPP):
+    """--one-process: the whole frame through nart_hip_render_device on a multi-device context
+    (the path the C ABI and the `nart` CLI ship): per-device host threads render their lattice
+    share of the buckets, the tiles are gathered to device 0 with the library's RCCL
+    ncclSend/ncclRecv group (device copies where RCCL is unavailable or the devices repeat), and
+    device 0 combines them.  The image stays on device 0 (no PCIe copy)."""
+    if "WORLD_SIZE" in os.environ and os.environ["WORLD_SIZE"] != "1":
+        print("bench.py: --one-process runs without a launcher", file=sys.stderr)
+        sys.exit(2)
+    same = os.environ.get("NART_BENCH_SAME_DEVICE", "0") not in ("", "0")
+    devices = [0] * a.gpus if same else list(range(a.gpus))
+    scene_dir = os.path.join("/tmp", "nart_bench_scene_%s_%d" % (a.config, os.getpid()))
+    path = cfg["scene"](scene_dir)
+    scene = nart_amd.Scene(path)
+    p = nart_amd.load_sessions(path)[0]
+    p.image_width, p.image_height, p.spp = W, H, SPP
+    g = nart_amd.session_geometry(p)
+    nb = g.n_buckets_x * g.n_buckets_y
+    torch.cuda.set_device(0)
+    gpu = nart_amd.HipRenderer(scene, devices=devices) if a.gpus > 1 else nart_amd.HipRenderer(scene, device=0)
+    gather = gpu.gather_mode() if a.gpus > 1 else "none"
+    for _ in range(a.warmup):
+        gpu.render_device(p)
+    torch.cuda.synchronize()
+    st = nart_amd.RenderStats()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        dptr = gpu.render_device(p, st)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    value = W * H * SPP * a.steps / dt / 1e6
+    n_img = g.total_height * g.total_width * 5
+    image = torch.empty(n_img, dtype=torch.float32, device="cuda:0")
+    # copy the context's device image into a torch tensor (device to device, after the timed steps)
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    rc = hip.hipMemcpy(ctypes.c_void_p(image.data_ptr()), ctypes.c_void_p(dptr), ctypes.c_size_t(n_img * 4),
+                       ctypes.c_int(3))  # hipMemcpyDeviceToDevice
+    assert rc == 0, rc
+    image = image.view(g.total_height, g.total_width, 5)
+    out = {
+        "metric": "Msamples/s at %dx%dx%dspp (%s)" % (W, H, SPP, os.path.basename(path)),
+        "value": round(value, 3), "unit": "Msamples/s", "n_gpus": a.gpus, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f32", "data": cfg["data"],
+        "config": {"workload": workload_name(cfg, a, W, H, SPP), "image": [W, H], "spp": SPP, "buckets": nb,
+                   "parallelism": "buckets on a lattice over %d device(s) of one process (nart_hip_create_multi)"
+                                  % a.gpus},
+        "gather": {"rccl": "library ncclSend/ncclRecv group to device 0 (nart_hip_create_multi, INTEGRATION.md 3a)",
+                   "copy": "device-to-device copies to device 0 (NART_GATHER=copy or repeated devices)",
+                   "copy-fallback": "device-to-device copies to device 0 (RCCL unavailable)",
+                   "none": "none (one device)"}[gather],
+        "devices": devices,
+        "kernel_ms_per_step": round(st.kernel_ms / a.steps, 3),
+        "splat_ms_per_step": round(st.splat_ms / a.steps, 3),
+        "latin_ms_per_step": round(st.latin_ms / a.steps, 3),
+        "schedule": st.schedule_names(),
+        "image_finite": bool(torch.isfinite(image).all().item()),
+    }
+    if a.dump_image:
+        np.save(a.dump_image, image.cpu().numpy())
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -161,11 +231,17 @@ def main():
     # smaller frames of the same scene (multi-rank rehearsals and tests; not a bench line)
     ap.add_argument("--size", default=None, help="WxHxSPP override, e.g. 320x180x8")
     ap.add_argument("--dump-image", default=None, help="rank 0 saves the combined float32 image (.npy)")
+    ap.add_argument("--one-process", action="store_true",
+                    help="one process drives all --gpus devices through the library's multi-device context "
+                         "(nart_hip_create_multi: per-device threads, RCCL ncclSend/ncclRecv gather to device 0, "
+                         "INTEGRATION.md 3a) instead of one rank per GPU")
     a = ap.parse_args()
     cfg = CONFIGS[a.config]
     W, H, SPP = cfg["w"], cfg["h"], cfg["spp"]
     if a.size:
         W, H, SPP = (int(v) for v in a.size.lower().split("x"))
+    if a.one_process:
+        return one_process_main(a, cfg, W, H, SPP)
 
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         # no launcher: start the N ranks here, before this process touches a GPU
@@ -290,9 +366,17 @@ def main():
     # moves is `traffic` (rocprofv3 2 x FETCH_SIZE + WRITE_SIZE per launch) -> measured_frac, and
     # what limits the kernel shows in lane_utilization (SQ_THREAD_CYCLES_VALU / 64
     # SQ_ACTIVE_INST_VALU: divergent lanes) and valu_busy.
+    # `bound` is the contract's ceiling class (no MFMA on this path, so "hbm"); `frac` is the
+    # contract's algorithmic fraction and is restated as `algorithmic_frac`, beside the measured
+    # `measured_frac`, so neither reads as the other.
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "frac_kind": "algorithmic: contract bytes (SURVEY.md 8(d)) / kernel time / HBM peak; most of those "
+                             "bytes are served by LDS/L1/L2, so this is NOT measured HBM utilisation "
+                             "(that is measured_frac)",
+                "algorithmic_frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "achieved_kind": "algorithmic bytes per launch (SURVEY.md 8(d) per-sample model x traced samples)",
+                "limiter_class": "latency",
                 "limiter": "latency/issue: dependent LDS/L2 loads in BVH traversal and divergent lanes "
                            "(DESIGN.md section 4), not HBM bandwidth",
                 "measured_frac": (round(traffic / (kernel_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
@@ -333,11 +417,13 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": cfg["data"],
-            "config": {"workload": cfg["workload"] if not a.size else "%s, resized to %dx%d %dspp (rehearsal, not "
-                                                                              "the bench workload)" % (
-                           cfg["workload"], W, H, SPP), "image": [W, H], "spp": SPP, "buckets": nb,
+            "config": {"workload": workload_name(cfg, a, W, H, SPP), "image": [W, H], "spp": SPP, "buckets": nb,
                        "parallelism": "buckets interleaved over %d rank(s), %s gather to rank 0" % (
                            world, {"nccl": "RCCL"}.get(backend, backend))},
+            "gather": ("none (one rank)" if world == 1 else
+                       "torch.distributed gather of the ranks' device tiles to rank 0 over %s, one process per GPU "
+                       "(nart_amd/dist.py BucketShard); the C ABI's multi-device context gathers with its own "
+                       "ncclSend/ncclRecv group instead (bench.py --one-process)" % {"nccl": "RCCL"}.get(backend, backend)),
             "roofline": roofline,
             "kernel_ms_per_step": round(st.kernel_ms / a.steps, 3),
             "splat_ms_per_step": round(st.splat_ms / a.steps, 3),

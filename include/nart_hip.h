@@ -33,7 +33,8 @@ typedef struct nart_render_stats {
     double kernel_ms;       /* device time of the path-tracing kernels (HIP events)     */
     double splat_ms;        /* device time of the splat + combine kernels               */
     uint32_t kernel_launches; /* number of path-tracing kernel launches timed in kernel_ms */
-    uint32_t reserved;
+    uint32_t schedule;      /* NART_SCHED_* bits: the scheduling paths the render took (OR over
+                               its launches; observability for tests and benches)         */
     uint64_t samples;       /* camera samples counted in the metric (W*H*spp share)     */
     uint64_t traced_samples;/* samples actually traced (incl. extra rows, render.cpp:164) */
     /* Counter pass only (nart_hip_set_counters(ctx,1)); zero otherwise.  bounces = extension
@@ -46,6 +47,16 @@ typedef struct nart_render_stats {
     double primary_ms;      /* part of kernel_ms: the camera-ray kernel that runs before the path
                                kernel (k_primary, default variant only)                  */
 } nart_render_stats;
+
+/* nart_render_stats.schedule bits */
+#define NART_SCHED_PROBE_QUEUE 0x1u  /* cost probe + pixel queue, persistent refill lanes          */
+#define NART_SCHED_PRIORITY    0x2u  /* priority lanes for the costliest pixels (ray-queue kernel) */
+#define NART_SCHED_SPEC_PAIRS  0x4u  /* speculative lane groups on the costliest pixels            */
+#define NART_SCHED_WAVE_GROUPS 0x8u  /* wave-group refill in probe order (ray-queue kernel)        */
+#define NART_SCHED_VOL_QUEUE   0x10u /* volume kernel: cost probe, costliest groups first          */
+#define NART_SCHED_VOL_SPARSE  0x20u /* volume kernel: sparse waves for the costliest groups       */
+#define NART_SCHED_SPLAT_SKEW  0x40u /* skewed-time splat (k_splat_skew)                           */
+#define NART_SCHED_PRIMARY     0x80u /* camera rays traced first (k_primary)                       */
 
 /* Upload the scene, build the device BVH.  device_id: HIP ordinal. */
 int nart_hip_create(const nart_scene_blob* scene, int device_id, nart_ctx** out);
@@ -87,6 +98,13 @@ int nart_hip_device_count(int* count);
 int nart_hip_shard_buckets(uint32_t n_buckets_x, uint32_t n_buckets, uint32_t n_devices, uint32_t device_index,
                            uint32_t* ids, uint32_t* count);
 
+/* Whole-session render into device memory: as nart_hip_render, but the combined image stays on
+   the (first) device, in a buffer the context owns (valid until the next render or destroy), and
+   *d_image points at it -- no PCIe copy.  Multi-device contexts gather the tiles to device 0 with
+   their RCCL send/receive group (or device copies) first.  Synchronous. */
+int nart_hip_render_device(nart_ctx* ctx, const nart_render_params* p, const nart_pixel** d_image,
+                           nart_render_stats* stats);
+
 /* Whole-session render, Render()-equivalent: fills a caller-owned host buffer of
    totalW*totalH nart_pixel (render.cpp:114-206 contract, render.h:18-21 layout). */
 int nart_hip_render(nart_ctx* ctx, const nart_render_params* p, nart_pixel* image,
@@ -126,6 +144,14 @@ int nart_hip_splat_thresholds(float filter_width, float* thr65);
    b0 + c, as {threshold t, weight below t, weight at or above t, 0} (at most one threshold per
    cell), cells4 with room for 2048 cells.  NART_E_INVALID where the thresholds do not apply. */
 int nart_hip_splat_lut(float filter_width, float* cells4, uint32_t* n_cells, uint32_t* b0);
+
+/* Environment-map CDF search (host only, no device; test hook for the guide tables of
+   path.h guided_search): for each of values[0, m), the reference's BinarySearch over v[0, n)
+   (util.cpp:4-20) into full[] and the guided search into guided[].  Returns 1 if a guide table
+   was built for v (non-decreasing, NaN-free, n < 2^16), 0 if not (the guided search is then the
+   full search), NART_E_INVALID on bad arguments. */
+int nart_hip_env_search(const float* v, uint32_t n, const float* values, uint32_t m, uint32_t* full,
+                        uint32_t* guided);
 
 /* Acceleration structure the context would build for a scene (host only, no device): BVH2 node
    count, traversal stack depth (levels; the device keeps 8 B per level per lane in LDS) and the

@@ -58,16 +58,24 @@ class BvhInfo(ctypes.Structure):
                 ("reserved", ctypes.c_uint32)]
 
 
+# nart_render_stats.schedule bits (include/nart_hip.h NART_SCHED_*)
+SCHED = {"probe_queue": 0x1, "priority": 0x2, "spec_pairs": 0x4, "wave_groups": 0x8, "vol_queue": 0x10,
+         "vol_sparse": 0x20, "splat_skew": 0x40, "primary": 0x80}
+
+
 class RenderStats(ctypes.Structure):
     _fields_ = [("render_ms", ctypes.c_double), ("kernel_ms", ctypes.c_double), ("splat_ms", ctypes.c_double),
-                ("kernel_launches", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("samples", ctypes.c_uint64),
+                ("kernel_launches", ctypes.c_uint32), ("schedule", ctypes.c_uint32), ("samples", ctypes.c_uint64),
                 ("traced_samples", ctypes.c_uint64), ("rays_extend", ctypes.c_uint64), ("rays_shadow", ctypes.c_uint64),
                 ("node_visits", ctypes.c_uint64), ("tri_tests", ctypes.c_uint64), ("bounces", ctypes.c_uint64),
                 ("latin_ms", ctypes.c_double), ("octree_checks", ctypes.c_uint64),
                 ("octree_replays", ctypes.c_uint64), ("primary_ms", ctypes.c_double)]
 
+    def schedule_names(self):
+        return sorted(k for k, v in SCHED.items() if self.schedule & v)
+
     def as_dict(self):
-        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+        return {f: getattr(self, f) for f, _ in self._fields_}
 
 
 _P = ctypes.c_void_p
@@ -83,7 +91,8 @@ class _BlobHead(ctypes.Structure):
     _fields_ = [("num_triangles", ctypes.c_uint32), ("num_meshes", ctypes.c_uint32),
                 ("num_materials", ctypes.c_uint32), ("num_lights", ctypes.c_uint32),
                 ("num_textures", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("triangles", _P),
-                ("meshes", _P), ("materials", _P), ("lights", _P), ("textures", ctypes.POINTER(_Texture))]
+                ("meshes", _P), ("materials", _P), ("lights", _P), ("textures", ctypes.POINTER(_Texture)),
+                ("cam_fov", ctypes.c_float), ("cam_m", ctypes.c_float * 16)]
 
 
 _SCENE_SIGS = {
@@ -110,6 +119,8 @@ _HIP_SIGS = {
     "nart_hip_destroy": (None, [_P]),
     "nart_hip_last_error": (ctypes.c_char_p, [_P]),
     "nart_hip_render": (ctypes.c_int, [_P, ctypes.POINTER(RenderParams), _P, ctypes.POINTER(RenderStats)]),
+    "nart_hip_render_device": (ctypes.c_int, [_P, ctypes.POINTER(RenderParams), ctypes.POINTER(_P),
+                                              ctypes.POINTER(RenderStats)]),
     "nart_hip_render_buckets_async": (ctypes.c_int, [_P, ctypes.POINTER(RenderParams), ctypes.POINTER(ctypes.c_uint32),
                                                      ctypes.c_uint32, _P, _P, ctypes.POINTER(RenderStats)]),
     "nart_hip_combine_async": (ctypes.c_int, [_P, ctypes.POINTER(RenderParams), _P, _P, _P]),
@@ -120,6 +131,7 @@ _HIP_SIGS = {
     "nart_hip_set_variant": (ctypes.c_int, [_P, ctypes.c_int]),
     "nart_hip_set_splat_mode": (ctypes.c_int, [_P, ctypes.c_int]),
     "nart_hip_splat_thresholds": (ctypes.c_int, [ctypes.c_float, _P]),
+    "nart_hip_env_search": (ctypes.c_int, [_P, ctypes.c_uint32, _P, ctypes.c_uint32, _P, _P]),
     "nart_hip_splat_lut": (ctypes.c_int, [ctypes.c_float, _P, ctypes.POINTER(ctypes.c_uint32),
                                           ctypes.POINTER(ctypes.c_uint32)]),
     "nart_hip_bvh_info": (ctypes.c_int, [_P, ctypes.POINTER(BvhInfo)]),
@@ -276,6 +288,11 @@ class Scene:
         return np.ctypeslib.as_array(ctypes.cast(h.triangles, ctypes.POINTER(ctypes.c_float)),
                                      shape=(h.num_triangles * 24,)).copy().reshape(-1, 24)
 
+    def camera(self):
+        """(fov, m): the camera's fov and glm::mat4 storage (16 float32; pinholecamera.cpp:3-40)."""
+        h = self._view()
+        return float(h.cam_fov), np.array(list(h.cam_m), np.float32)
+
     def textures(self):
         """Loaded textures as (H, W, 4) uint16 half bit patterns (top row first), in load order."""
         h = self._view()
@@ -382,6 +399,15 @@ class HipRenderer:
         st = stats if stats is not None else RenderStats()
         self._check(self._lib.nart_hip_render(self._ctx, ctypes.byref(p), img.ctypes.data, ctypes.byref(st)))
         return img
+
+    def render_device(self, p, stats=None):
+        """Whole session, image left on the (first) device: returns its device address (totalH x
+        totalW x 5 float32, owned by the context until the next render).  Multi-device contexts
+        gather over their RCCL send/receive group first (nart_hip_render_device)."""
+        st = stats if stats is not None else RenderStats()
+        ptr = _P()
+        self._check(self._lib.nart_hip_render_device(self._ctx, ctypes.byref(p), ctypes.byref(ptr), ctypes.byref(st)))
+        return ptr.value
 
     def render_buckets_async(self, p, bucket_ids, d_tiles_ptr, stream_ptr=0, stats=None):
         ids = np.ascontiguousarray(bucket_ids, dtype=np.uint32)

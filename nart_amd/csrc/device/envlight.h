@@ -14,7 +14,7 @@ ND float env_ptn_pdf(const DScene& S, const DLight& L, f2 st) {
     return env_pdf(S.envs[L.env], F2(gmin(st.x, 0.9999f), gmin(st.y, 0.9999f)));
 }
 
-// Light::Li (disklight.cpp:12-23, ringlight.cpp:117-128, environmentlight.cpp:9-28).
+// Light::Li (disklight.cpp:12-23, ringlight.cpp:13-24, environmentlight.cpp:9-28).
 // ENV = false compiles the environment branch out (scenes without one): it costs registers.
 // theta_in: acosf(wi.z) already formed by the caller (k_render_volume_sm shares that evaluation
 // with its scattering phase), or NAN to form it here
@@ -58,7 +58,7 @@ ND void light_bound(const DLight& L, f3 p, f3 wi, float& tMax) {
     (void)area_pdf(L, p, wi, st, tMax);
 }
 
-// Light::Sample_Li (disklight.cpp:25-60, ringlight.cpp:130-168)
+// Light::Sample_Li (disklight.cpp:25-60, ringlight.cpp:26-64)
 template <bool ENV = true>
 ND f3 light_sample_li(const DScene& S, const DLight& L, f3 p, f3& wi, f2 sample, float& pdf, float& tMax) {
     if (ENV && L.type == NART_LIGHT_ENVIRONMENT) {

@@ -1053,6 +1053,8 @@ __global__ __launch_bounds__(256) void k_primary(DScene S, RenderArgs A, uint32_
 // shard; the frame is unchanged (bit-identical).
 #define RQ_PENDING 0xFFFFFFFEu
 #define RQ_RING 256u
+#define RQ_CHAIN_OFF (24 + 8 * 70000 + 4200000)  // NART_WAVEPROF chain records: 8 words per lane
+#define RQ_CHAIN_MAX 262144u                      // lanes with a record
 NHD size_t rq_lds_bytes(uint32_t stack_depth, uint32_t block) {
     const uint32_t waves = block / 64;
     return (size_t)stack_depth * block * 8 + (size_t)waves * 3 * 64 * 32 + (size_t)block * 16 +
@@ -1179,6 +1181,15 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
         prof_sec[i] += _n - prof_last;                             \
         prof_last = _n;                                            \
     } while (0)
+    // critical-path record of the lane's first pixel (its chain): shader cycles with its own rays
+    // in flight, with its rays resolved while the traversal phase serves other lanes, in path
+    // phases where it shaded or started samples, in path phases where it did not, and otherwise
+    // (RQ_CHAIN_OFF records, render.hip prints the last-finishing chains)
+    bool cp_on = slot != 0xFFFFFFFFu;
+    const uint32_t cp_slot = slot;
+    const bool cp_prio = prio, cp_pm = pm;
+    uint64_t cp_tr = 0, cp_wait = 0, cp_shade = 0, cp_other = 0, cp_idle = 0;
+    bool cp_did = false;
 #else
 #define RQ_MARK(i) ((void)0)
 #endif
@@ -1244,6 +1255,7 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
         if (COUNT && lane == 0) cnt.pw[10]++;  // path phases
         const uint64_t prof_tp = __builtin_amdgcn_s_memtime();
         prof_last = prof_tp;
+        cp_did = false;
 #endif
         // 1. results of lanes whose queries are all in: EstimateDirect term, then the hit to
         //    shade or the end of the sample
@@ -1403,6 +1415,22 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
             }
         }
         RQ_MARK(0);
+#ifdef NART_WAVEPROF
+        if (cp_on && !pm && s >= A.spp && !waiting && gid < RQ_CHAIN_MAX) {
+            // the first pixel's chain is done: its record (the path phase so far counts as its own)
+            cp_shade += __builtin_amdgcn_s_memtime() - prof_tp;
+            unsigned long long* rec = A.counters + RQ_CHAIN_OFF + 8 * (size_t)gid;
+            rec[0] = (unsigned long long)cp_slot | (cp_prio ? 1ull << 32 : 0ull) | (cp_pm ? 1ull << 33 : 0ull) | (1ull << 34);
+            rec[1] = __builtin_amdgcn_s_memrealtime() - prof_rt0;
+            rec[2] = cp_tr;
+            rec[3] = cp_wait;
+            rec[4] = cp_shade;
+            rec[5] = cp_other;
+            rec[6] = cp_idle;
+            rec[7] = __builtin_amdgcn_s_memtime() - prof_t0;
+            cp_on = false;
+        }
+#endif
         // pixel refill (persistent grid): one queue atomic per wave
         if (A.qhead) {
             const bool need = !pm && !waiting && s >= A.spp && slot != 0xFFFFFFFEu;
@@ -1443,6 +1471,9 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
         //    k_primary found to escape, or a zero bounce limit, ends its sample here, so loop until
         //    a hit is to be shaded, a ray is queued or the pixel is done.
         while (active) {
+#ifdef NART_WAVEPROF
+            cp_did = true;
+#endif
             nd = 0;
             // pixel-major rows (stride 1): samples and camera hits are read in pairs, the odd one
             // kept for the lane's next sample -- each read of a line the lane's neighbours do not
@@ -1511,6 +1542,9 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
         RQ_MARK(2);
         // 3. shade the hits (pathintegrator.cpp:185-246)
         if (need_shade) {
+#ifdef NART_WAVEPROF
+            cp_did = true;
+#endif
             if (COUNT) ++n_bounce;
             if (COUNT) WPROF(cnt, 8);
             const float4 ro = my_out[lane * 2], rd = my_out[lane * 2 + 1];
@@ -1664,6 +1698,11 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
         // ---------------- traversal phase: lanes take the wave's queued rays in turn
 #ifdef NART_WAVEPROF
         const uint64_t prof_tt = __builtin_amdgcn_s_memtime();
+        if (cp_on) {
+            if (cp_did) cp_shade += prof_tt - prof_tp;
+            else cp_other += prof_tt - prof_tp;
+        }
+        uint64_t cp_last = prof_tt;
 #endif
         for (;;) {
             const bool need = !tracing;
@@ -1709,6 +1748,20 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                 const uint32_t kind = tid8 >> 6;
                 rw[kind] = kind == 0u ? bg : (bg != NO_HIT ? 1u : 0u);
             }
+#ifdef NART_WAVEPROF
+            if (cp_on) {
+                const uint64_t now = __builtin_amdgcn_s_memtime();
+                if (waiting) {
+                    const uint4 r = *my_res;
+                    const bool in = (!ext_pending || r.x != RQ_PENDING) && (!use1 || r.y != 2u) && (!use2 || r.z != 2u);
+                    if (in) cp_wait += now - cp_last;
+                    else cp_tr += now - cp_last;
+                } else {
+                    cp_idle += now - cp_last;
+                }
+                cp_last = now;
+            }
+#endif
             // priority rays all resolved and a priority lane waits on its results: shade it now
             if (A.rq_prio && ph == pt && __ballot(tracing && tr_prio) == 0 && __ballot(waiting && prio) != 0) break;
             if (ph == pt && nh == nt && (uint32_t)__popcll(__ballot(tracing)) <= A.rq_quorum) break;

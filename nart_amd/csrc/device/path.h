@@ -1049,7 +1049,7 @@ ND void create_bsdf(const DScene& S, const Isect& is, float alphaTweak, BSDF& bs
 }
 
 // ---------------------------------------------------------------- lights
-ND uint32_t binary_search(float value, const float* v, uint32_t start, uint32_t end) {  // util.cpp:4-20
+NHD uint32_t binary_search(float value, const float* v, uint32_t start, uint32_t end) {  // util.cpp:4-20
     uint32_t i = start;
     while (start < end) {
         i = start + ((end - start) / 2);
@@ -1066,9 +1066,10 @@ ND uint32_t binary_search(float value, const float* v, uint32_t start, uint32_t 
 // [start, end) with v[j] > value (end if none), whichever probes it takes; ub is monotone in value,
 // so for value in guide cell c it lies in [a_c, b_c] (the bounds of the cell's end values, build_env)
 // and a search of that range finds the same ub.  Two or three dependent loads instead of ~10.
-ND uint32_t guided_search(float value, const float* v, uint32_t start, uint32_t end, const uint32_t* guide) {
+NHD uint32_t guided_search(float value, const float* v, uint32_t start, uint32_t end, const uint32_t* guide) {
     if (!guide || start >= end || !(value >= 0.f)) return binary_search(value, v, start, end);
-    const uint32_t c = min(NART_ENV_GUIDE_K - 1u, f2u32(value * (float)NART_ENV_GUIDE_K));
+    const uint32_t c0 = f2u32(value * (float)NART_ENV_GUIDE_K);
+    const uint32_t c = c0 < NART_ENV_GUIDE_K - 1u ? c0 : NART_ENV_GUIDE_K - 1u;
     const uint32_t g = guide[c];
     uint32_t lo = start + (g & 0xFFFFu), hi = start + (g >> 16);
     while (lo < hi) {
@@ -1101,7 +1102,7 @@ ND f2 env_sample(const DEnvDist& d, f2 s, float& pdf) {  // texturepattern.cpp:7
     return F2(uc, vc);
 }
 
-// Disk / ring Pdf (disklight.cpp:62-104, ringlight.cpp:170-216); sets st and tMax on a hit.
+// Disk / ring Pdf (disklight.cpp:62-104, ringlight.cpp:66-112); sets st and tMax on a hit.
 ND float area_pdf(const DLight& L, f3 p, f3 wi, f2& st, float& tMax) {
     f3 n = load3(L.n);
     if (dot(wi, n) >= 0.f) return 0.f;

@@ -117,6 +117,7 @@ void merge_stats(nart_render_stats& out, const nart_render_stats& s) {
     out.latin_ms = std::max(out.latin_ms, s.latin_ms);
     out.primary_ms = std::max(out.primary_ms, s.primary_ms);
     out.kernel_launches = std::max(out.kernel_launches, s.kernel_launches);
+    out.schedule |= s.schedule;
     out.samples += s.samples;
     out.traced_samples += s.traced_samples;
     out.rays_extend += s.rays_extend;
@@ -139,7 +140,8 @@ int ensure_dev(nart_ctx* ctx, int dev, void*& buf, size_t& cap, size_t bytes, co
     return NART_OK;
 }
 
-// Render(), multi-device: shard, render concurrently, gather to device 0, combine, copy out.
+// Render(), multi-device: shard, render concurrently, gather to device 0, combine, copy out (image
+// null: the combined image stays in ctx->d_image on device 0, nart_hip_render_device).
 int render_multi(nart_ctx* ctx, const nart_render_params* p, nart_pixel* image, nart_render_stats* stats) {
     const uint32_t n = (uint32_t)ctx->subs.size();
     if (ctx->rccl_broken)
@@ -212,12 +214,16 @@ int render_multi(nart_ctx* ctx, const nart_render_params* p, nart_pixel* image, 
         };
         note(R.GroupStart(), "ncclGroupStart");
         if (first == ncclSuccess) {
-            // test hook (nart_hip_debug_fault 1): the last device sends to a rank that does not exist
+            // test hook (nart_hip_debug_fault 1): the last device that owns buckets sends to a rank
+            // that does not exist, after the receives of the devices before it are posted
+            uint32_t last = n;
+            for (uint32_t d = 0; d < n; ++d)
+                if (!ids[d].empty()) last = d;
             const int bad_peer = ctx->debug_fault == 1 ? (int)n : 0;
             for (uint32_t d = 0; d < n; ++d) {
                 if (ids[d].empty()) continue;
                 const size_t cnt = ids[d].size() * tile_floats;
-                note(R.Send(ctx->sub_tiles[d], cnt, ncclFloat32, d + 1 == n ? bad_peer : 0, ctx->comms[d], ctx->streams[d]),
+                note(R.Send(ctx->sub_tiles[d], cnt, ncclFloat32, d == last ? bad_peer : 0, ctx->comms[d], ctx->streams[d]),
                      "ncclSend");
                 note(R.Recv(slabs + first_b[d] * tile_floats, cnt, ncclFloat32, (int)d, ctx->comms[0], s0), "ncclRecv");
             }
@@ -259,7 +265,7 @@ int render_multi(nart_ctx* ctx, const nart_render_params* p, nart_pixel* image, 
     if ((rc = nart_hip_combine_async(ctx->subs[0], p, static_cast<const nart_pixel*>(ctx->d_byid),
                                      static_cast<nart_pixel*>(ctx->d_image), s0)))
         return fail(ctx, rc, ctx->subs[0]->err);
-    HIPCHK(hipMemcpyAsync(image, ctx->d_image, img_bytes, hipMemcpyDeviceToHost, s0));
+    if (image) HIPCHK(hipMemcpyAsync(image, ctx->d_image, img_bytes, hipMemcpyDeviceToHost, s0));
     HIPCHK(hipStreamSynchronize(s0));
     if (stats) {
         nart_render_stats m;
@@ -270,6 +276,7 @@ int render_multi(nart_ctx* ctx, const nart_render_params* p, nart_pixel* image, 
         stats->latin_ms += m.latin_ms;
         stats->primary_ms += m.primary_ms;
         stats->kernel_launches += m.kernel_launches;
+        stats->schedule |= m.schedule;
         stats->samples += m.samples;
         stats->traced_samples += m.traced_samples;
         stats->rays_extend += m.rays_extend;

@@ -69,6 +69,7 @@ struct nart_ctx {
     size_t cap_slots = 0, cap_samples = 0, cap_buckets = 0;
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // ev[4]: after k_primary
     bool primary_ran = false;  // the last dispatch launched k_primary (ev[4] recorded)
+    uint32_t sched = 0;        // NART_SCHED_* bits of the current render (nart_render_stats::schedule)
     bool events = false;
     // megakernel work queue (launch_render)
     uint32_t* d_queue = nullptr;
@@ -172,6 +173,25 @@ DLight dlight(const nart_light& L) {
     return d;
 }
 
+// Guide table of one BinarySearch range v[0, n) (path.h guided_search): for each of the K cells of
+// values [c/K, (c+1)/K) the range [ub(c/K), ub(last float of the cell)] of the upper bound (first
+// index with v[j] > value), 16 bits each.  Only for non-decreasing, NaN-free ranges of < 2^16
+// entries; otherwise false and the device runs the full search.
+bool env_guide(const float* v, uint32_t n, uint32_t* out) {
+    const uint32_t K = NART_ENV_GUIDE_K;
+    if (n > 65535u) return false;
+    for (uint32_t j = 0; j + 1 < n; ++j)
+        if (!(v[j] <= v[j + 1])) return false;
+    if (n && v[0] != v[0]) return false;
+    auto ub = [&](float x) { return (uint32_t)(std::upper_bound(v, v + n, x) - v); };
+    for (uint32_t c = 0; c < K; ++c) {
+        const float lo = (float)c / (float)K;
+        const float hi = c + 1 == K ? INFINITY : std::nextafter((float)(c + 1) / (float)K, 0.f);
+        out[c] = ub(lo) | (ub(hi) << 16);
+    }
+    return true;
+}
+
 // Piecewise2DDistribution of an environment texture (texturepattern.cpp:3-70): marginal pdf of
 // the rows (top row last), conditional pdf per row, and their CDFs, with the reference's float
 // operation order.  Built on the host once per context.
@@ -218,18 +238,7 @@ int build_env(nart_ctx* ctx, const nart_texture& t, DEnvDist& d) {
     // the range [ub(c/K), ub(last float of the cell)] of the upper bound; built only over searched
     // ranges that are non-decreasing and NaN-free (otherwise the full search runs)
     const uint32_t K = NART_ENV_GUIDE_K;
-    auto guide = [&](const float* v, uint32_t n, uint32_t* out) {
-        for (uint32_t j = 0; j + 1 < n; ++j)
-            if (!(v[j] <= v[j + 1])) return false;
-        if (n && v[0] != v[0]) return false;
-        auto ub = [&](float x) { return (uint32_t)(std::upper_bound(v, v + n, x) - v); };
-        for (uint32_t c = 0; c < K; ++c) {
-            const float lo = (float)c / (float)K;
-            const float hi = c + 1 == K ? INFINITY : std::nextafter((float)(c + 1) / (float)K, 0.f);
-            out[c] = ub(lo) | (ub(hi) << 16);
-        }
-        return true;
-    };
+    auto guide = env_guide;
     std::vector<uint32_t> mguide(K), cguide((size_t)K * H);
     bool guided = W <= 65535 && H <= 65535 && guide(mcdf.data(), H, mguide.data());
     for (uint32_t j = 0; guided && j < H; ++j) guided = guide(ccdf.data() + (size_t)j * (W + 1), W, cguide.data() + (size_t)j * K);
@@ -641,6 +650,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             HIPCHK(hipEventRecord(ctx->ev[4], st));
             ctx->primary_ran = true;
         }
+        ctx->sched |= NART_SCHED_PRIMARY;
         brq.prim = ctx->d_prim;
     }
     brq.lds_nodes = render_lds_nodes(ctx, rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK), NART_RQ_BLOCK / 256);
@@ -707,6 +717,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                     // waves were still running (WAVEPROF timeline).  C3 frame 445 -> 407 ms
                     // (probe included; order 1: 408, top 20 / 35 %: 408 / 408 ms)
                     const int order = std::getenv("NART_RQ_ORDER") ? std::atoi(std::getenv("NART_RQ_ORDER")) : 2;
+                    ctx->sched |= NART_SCHED_WAVE_GROUPS;
                     if (order == 1 || order == 2) {
                         RenderArgs pb = b;  // cost probe: the first sample of every pixel
                         pb.spp = 1;
@@ -783,11 +794,14 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                 b.rq_prio = pbit ? 1u : 0u;
                 b.rq_pairs = pairs;
                 b.qlen = qlen;
+                if (pbit) ctx->sched |= NART_SCHED_PRIORITY;
+                if (pairs) ctx->sched |= NART_SCHED_SPEC_PAIRS;
             }
             b.queue = ctx->d_queue;
             if (refill) {
                 HIPCHK(hipMemsetAsync(ctx->d_qhead, 0, sizeof(uint32_t), st));
                 b.qhead = ctx->d_qhead;
+                ctx->sched |= NART_SCHED_PROBE_QUEUE;
                 // whole ray-queue blocks, so that every first-round lane's entry lies below qbase
                 const uint32_t per = rq ? NART_RQ_BLOCK / 256 : 1u;
                 blocks = (resident + per - 1u) / per * per;
@@ -852,6 +866,7 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             rc = sort_groups_by_cost(ctx, n, ctx->d_queue, st);
             if (rc) return rc;
             b.queue = ctx->d_queue;
+            ctx->sched |= NART_SCHED_VOL_QUEUE;
             // Sparse waves on shards of < NART_VOL_SPARSE_ROUNDS (default 2) rounds of resident
             // waves: the costliest groups (probe cost >= NART_VOL_SPARSE_F (4) x the median group's)
             // spread NART_VOL_SPARSE (16) pixels per wave, the other lanes idle.  A wave executes
@@ -885,6 +900,7 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                                        qlen, ctx->d_queue);
                     b.qlen = qlen;
                     grid = (qlen + 255) / 256;
+                    ctx->sched |= NART_SCHED_VOL_SPARSE;
                 }
             }
             HIPCHK(hipGetLastError());
@@ -1030,6 +1046,51 @@ int launch_latin(nart_ctx* ctx, const RenderArgs& ra, hipStream_t st) {
     return NART_OK;
 }
 
+#ifdef NART_WAVEPROF
+// k_render_rq chain records (NART_WAVEPROF builds, NART_CHAIN_REPORT set; development profile)
+int chain_report(nart_ctx* ctx, const std::vector<uint32_t>& xy) {
+    // k_render_rq chain records (first pixel of each lane): the last-finishing chains'
+    // critical-path split, shader cycles: own rays outstanding (queued or traced) / own rays
+    // resolved while the traversal phase serves others / path phases in which it shaded
+    // or started samples / path phases of other lanes / lane idle in traversal
+    std::vector<unsigned long long> r(8 * (size_t)RQ_CHAIN_MAX);
+    HIPCHK(hipMemcpy(r.data(), ctx->d_counters + RQ_CHAIN_OFF, r.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<std::pair<unsigned long long, uint32_t>> fin;
+    double sum[6] = {0, 0, 0, 0, 0, 0}, psum[6] = {0, 0, 0, 0, 0, 0};
+    uint32_t np = 0;
+    for (uint32_t i = 0; i < RQ_CHAIN_MAX; ++i)
+        if (r[8 * i] >> 34) {
+            fin.push_back({r[8 * i + 1], i});
+            const bool pr = (r[8 * i] >> 32) & 1u;
+            for (int k = 0; k < 6; ++k) {
+                const double v = (double)r[8 * i + 2 + k];
+                sum[k] += v;
+                if (pr) psum[k] += v;
+            }
+            np += pr ? 1u : 0u;
+        }
+    std::sort(fin.begin(), fin.end());
+    const double n = (double)std::max<size_t>(1, fin.size());
+    fprintf(stderr, "CHAIN records %zu (priority %u) mean cycles: own_rays %.0f wait_others %.0f shade %.0f "
+                    "other_path %.0f idle %.0f total %.0f\n", fin.size(), np, sum[0] / n, sum[1] / n, sum[2] / n,
+            sum[3] / n, sum[4] / n, sum[5] / n);
+    if (np)
+        fprintf(stderr, "CHAIN priority mean cycles: own_rays %.0f wait_others %.0f shade %.0f other_path %.0f "
+                        "idle %.0f total %.0f\n", psum[0] / np, psum[1] / np, psum[2] / np, psum[3] / np,
+                psum[4] / np, psum[5] / np);
+    for (size_t k = 0; k < 8 && k < fin.size(); ++k) {
+        const uint32_t i = fin[fin.size() - 1 - k].second;
+        const unsigned long long* q = &r[8 * (size_t)i];
+        const uint32_t sl = (uint32_t)(q[0] & 0xFFFFFFFFu);
+        fprintf(stderr, "CHAIN last#%zu lane %u slot %u px (%u,%u) prio %d pair %d finish %.3f ms cycles: own_rays "
+                        "%llu wait_others %llu shade %llu other_path %llu idle %llu total %llu\n",
+                k, i, sl, sl < xy.size() ? xy[sl] & 0xFFFFu : 0u, sl < xy.size() ? xy[sl] >> 16 : 0u,
+                (int)((q[0] >> 32) & 1u), (int)((q[0] >> 33) & 1u), q[1] * 1e-5, q[2], q[3], q[4], q[5], q[6], q[7]);
+    }
+    return NART_OK;
+}
+#endif
+
 // Render a bucket list into device tiles (list order).  Shared by all entry points.
 int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* ids, uint32_t n, float* d_tiles,
                    hipStream_t st, nart_render_stats* stats) {
@@ -1083,12 +1144,16 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         HIPCHK(hipMemcpy(ctx->d_lut, lut.data(), lut.size() * sizeof(float4), hipMemcpyHostToDevice));
     }
 #ifdef NART_WAVEPROF
-    const size_t n_cnt = 24 + 8 * 70000 + 4200000;  // + per-wave and per-slot records (development profile)
+    // + per-wave and per-slot records, + k_render_rq chain records (development profile)
+    const size_t n_cnt = RQ_CHAIN_OFF + 8 * (size_t)RQ_CHAIN_MAX;
 #else
     const size_t n_cnt = 24;
 #endif
     if (!ctx->d_counters) HIPCHK(hipMalloc(&ctx->d_counters, n_cnt * sizeof(unsigned long long)));
     if (ctx->counters) HIPCHK(hipMemsetAsync(ctx->d_counters, 0, n_cnt * sizeof(unsigned long long), st));
+#ifdef NART_WAVEPROF
+    else HIPCHK(hipMemsetAsync(ctx->d_counters + RQ_CHAIN_OFF, 0, 8 * (size_t)RQ_CHAIN_MAX * 8, st));
+#endif
     if (!ctx->events) {
         for (auto& e : ctx->ev) HIPCHK(hipEventCreate(&e));
         ctx->events = true;
@@ -1099,6 +1164,7 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
     uint32_t launches = 0;
     uint64_t traced = 0, counted = 0;
     uint32_t b0 = 0;
+    ctx->sched = 0;
     std::vector<uint32_t> xy, base;
     while (b0 < n) {
         // gather a batch of buckets whose traced pixels fit the slot budget
@@ -1190,6 +1256,7 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         // splat modes (all bit-identical, mode 3 the default): 3 four tile pixels per lane; 2 / 1 / 0
         // one tile pixel per lane with the compare-only / threshold / direct filter-index arithmetic
         if (skew) {
+            ctx->sched |= NART_SCHED_SPLAT_SKEW;
             const uint32_t nb = skew_bands;  // tile-row bands per bucket (k_splat_skew's NB)
             const uint32_t pb = 64u / g.tile_size, nblk = (nbk * nb + 4 * pb - 1) / (4 * pb);
             const size_t lds = lut.size() * sizeof(float4) + 8u * pb * sizeof(uint32_t);
@@ -1226,6 +1293,9 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         splat_ms += ms;
         HIPCHK(hipEventElapsedTime(&ms, ctx->ev[3], ctx->ev[0]));
         latin_ms += ms;
+#ifdef NART_WAVEPROF
+        if (std::getenv("NART_CHAIN_REPORT") && (rc = chain_report(ctx, xy))) return rc;
+#endif
         ++launches;
         b0 = b1;
     }
@@ -1235,6 +1305,7 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         stats->latin_ms += latin_ms;
         stats->primary_ms += primary_ms;
         stats->kernel_launches += launches;
+        stats->schedule |= ctx->sched;
         stats->traced_samples += traced;
         stats->samples += counted * p->spp;
         if (ctx->counters) {
@@ -1671,6 +1742,8 @@ void nart_hip_destroy(nart_ctx* ctx) {
                     ctx->d_qhead, ctx->d_sort_tmp};
     for (void* b : bufs)
         if (b) hipFree(b);
+    for (void* b : {ctx->d_gather, ctx->d_image})  // nart_hip_render_device's tiles and image
+        if (b) hipFree(b);
     for (void* b : ctx->env_bufs) hipFree(b);
     if (ctx->events)
         for (auto& e : ctx->ev) hipEventDestroy(e);
@@ -1780,6 +1853,37 @@ int nart_hip_render(nart_ctx* ctx, const nart_render_params* p, nart_pixel* imag
     return rc;
 }
 
+int nart_hip_render_device(nart_ctx* ctx, const nart_render_params* p, const nart_pixel** d_image,
+                           nart_render_stats* stats) {
+    if (!ctx || !p || !d_image) return NART_E_INVALID;
+    auto t0 = std::chrono::steady_clock::now();
+    int rc = NART_OK;
+    if (!ctx->subs.empty()) {
+        rc = render_multi(ctx, p, nullptr, stats);  // tiles gathered to device 0, combined there
+        if (!rc) *d_image = static_cast<const nart_pixel*>(ctx->d_image);
+    } else {
+        if ((rc = check_params(ctx, p))) return rc;
+        HIPCHK(hipSetDevice(ctx->device));
+        nart_session_geometry g;
+        nart_session_geometry_of(p, &g);
+        const uint32_t nb = g.n_buckets_x * g.n_buckets_y;
+        std::vector<uint32_t> ids(nb);
+        for (uint32_t i = 0; i < nb; ++i) ids[i] = i;
+        const size_t tile_bytes = (size_t)nb * g.tile_size * g.tile_size * sizeof(nart_pixel);
+        const size_t img_bytes = (size_t)g.total_width * g.total_height * sizeof(nart_pixel);
+        if ((rc = ensure_dev(ctx, ctx->device, ctx->d_gather, ctx->cap_gather, tile_bytes, "tiles")) ||
+            (rc = ensure_dev(ctx, ctx->device, ctx->d_image, ctx->cap_image, img_bytes, "image")))
+            return rc;
+        rc = render_buckets(ctx, p, ids.data(), nb, static_cast<float*>(ctx->d_gather), 0, stats);
+        if (!rc) rc = nart_hip_combine_async(ctx, p, static_cast<const nart_pixel*>(ctx->d_gather),
+                                            static_cast<nart_pixel*>(ctx->d_image), 0);
+        if (!rc && hipStreamSynchronize(0) != hipSuccess) rc = fail(ctx, NART_E_HIP, "render");
+        if (!rc) *d_image = static_cast<const nart_pixel*>(ctx->d_image);
+    }
+    if (stats) stats->render_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
 int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t x0, uint32_t y0, uint32_t w,
                             uint32_t h, float* out) {
     if (!ctx || !p || !out) return NART_E_INVALID;
@@ -1802,12 +1906,15 @@ int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t
     HIPCHK(hipMemcpy(ctx->d_slot_xy, xy.data(), (size_t)n * 4, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(k_slot_rows, dim3((n + 255) / 256), dim3(256), 0, 0, n, p->spp, ctx->d_slot_so);
 #ifdef NART_WAVEPROF
-    const size_t n_cnt = 24 + 8 * 70000 + 4200000;  // as the bucket path (development profile)
+    const size_t n_cnt = RQ_CHAIN_OFF + 8 * (size_t)RQ_CHAIN_MAX;  // as the bucket path (development profile)
 #else
     const size_t n_cnt = 24;
 #endif
     if (!ctx->d_counters) HIPCHK(hipMalloc(&ctx->d_counters, n_cnt * sizeof(unsigned long long)));
     if (ctx->counters) HIPCHK(hipMemset(ctx->d_counters, 0, n_cnt * sizeof(unsigned long long)));
+#ifdef NART_WAVEPROF
+    else HIPCHK(hipMemset(ctx->d_counters + RQ_CHAIN_OFF, 0, 8 * (size_t)RQ_CHAIN_MAX * 8));
+#endif
     RenderArgs ra;
     ra.slot_xy = ctx->d_slot_xy;
     ra.slot_so = ctx->d_slot_so;
@@ -1864,6 +1971,7 @@ int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t
     }
     HIPCHK(hipMemcpy(out, ctx->d_L, (size_t)n * p->spp * sizeof(float4), hipMemcpyDeviceToHost));
 #ifdef NART_WAVEPROF
+    if (std::getenv("NART_CHAIN_REPORT") && (rc = chain_report(ctx, xy))) return rc;
     if (ctx->counters) {
         unsigned long long c[24], sc[8];
         HIPCHK(hipMemcpy(c, ctx->d_counters, sizeof(c), hipMemcpyDeviceToHost));
@@ -1891,6 +1999,18 @@ int nart_hip_bvh_info(const nart_scene_blob* blob, nart_bvh_info* out) {
     out->num_leaf_tris = bvh.num_leaf_tris;
     out->reserved = 0;
     return NART_OK;
+}
+
+int nart_hip_env_search(const float* v, uint32_t n, const float* values, uint32_t m, uint32_t* full,
+                        uint32_t* guided) {
+    if (!v || !values || !full || !guided || !n) return NART_E_INVALID;
+    std::vector<uint32_t> g(NART_ENV_GUIDE_K);
+    const bool ok = env_guide(v, n, g.data());
+    for (uint32_t i = 0; i < m; ++i) {
+        full[i] = binary_search(values[i], v, 0, n);
+        guided[i] = guided_search(values[i], v, 0, n, ok ? g.data() : nullptr);
+    }
+    return ok ? 1 : 0;
 }
 
 int nart_hip_splat_lut(float filter_width, float* cells4, uint32_t* n_cells, uint32_t* b0) {

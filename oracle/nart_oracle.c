@@ -969,7 +969,7 @@ static float ptn_pdf(const oracle_scene* s, int light, const nart_pattern* p, v2
 
 typedef struct { v3 p; v2 st; float tMax; } lisect_t;
 
-static float area_pdf(const nart_light* L, lisect_t* li, v3 p, v3 wi) { /* disklight.cpp:62-104, ringlight.cpp:170-216 */
+static float area_pdf(const nart_light* L, lisect_t* li, v3 p, v3 wi) { /* disklight.cpp:62-104, ringlight.cpp:66-112 */
     v3 center = xyz(vec_mul_mat(V4(0.f, 0.f, 0.f, 1.f), L->m));
     v3 n = xyz(vec_mul_mat(V4(0.f, 0.f, -1.f, 0.f), L->m));
     if (dot3(wi, n) >= 0.f) return 0.f;
@@ -1004,7 +1004,7 @@ static void env_dir(v3 wi, float* theta, float* phi) {
     if (*phi < 0.f) *phi += TWO_PI_F;
 }
 
-/* Light::Li (disklight.cpp:12-23, ringlight.cpp:117-128, environmentlight.cpp:9-28) */
+/* Light::Li (disklight.cpp:12-23, ringlight.cpp:13-24, environmentlight.cpp:9-28) */
 static v3 light_li(const oracle_scene* s, int li_idx, lisect_t* li, v3 p, v3 wi, float* pdf) {
     const nart_light* L = &s->blob->lights[li_idx];
     if (L->type == NART_LIGHT_ENVIRONMENT) {
@@ -1026,7 +1026,7 @@ static v3 light_li(const oracle_scene* s, int li_idx, lisect_t* li, v3 p, v3 wi,
     return V3(0.f, 0.f, 0.f);
 }
 
-/* Light::Sample_Li (disklight.cpp:25-60, ringlight.cpp:130-168, environmentlight.cpp:30-61) */
+/* Light::Sample_Li (disklight.cpp:25-60, ringlight.cpp:26-64, environmentlight.cpp:30-61) */
 static v3 light_sample_li(const oracle_scene* s, int li_idx, lisect_t* li, v3 p, v3* wi, v2 sample, float* pdf) {
     const nart_light* L = &s->blob->lights[li_idx];
     if (L->type == NART_LIGHT_ENVIRONMENT) {

@@ -159,3 +159,46 @@ def test_splat_weight_cells_reproduce_filter_weight(built):
         e = cells[c]
         got = np.where(d2 >= e[:, 0], e[:, 2], e[:, 1])
         assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), fw
+
+
+def _env_search(v, values):
+    import numpy as np
+    lib = nart_amd.api.hip_lib()
+    v = np.ascontiguousarray(v, np.float32)
+    values = np.ascontiguousarray(values, np.float32)
+    full = np.zeros(len(values), np.uint32)
+    guided = np.zeros(len(values), np.uint32)
+    rc = lib.nart_hip_env_search(v.ctypes.data, len(v), values.ctypes.data, len(values), full.ctypes.data,
+                                 guided.ctypes.data)
+    assert rc >= 0
+    return rc == 1, full, guided
+
+
+def test_env_guided_search_matches_binary_search(built):
+    """The environment light's guided CDF search (path.h guided_search + render.hip env_guide,
+    ADVICE r04) returns BinarySearch's index (util.cpp:4-20) for every value: regular CDFs,
+    plateaus (zero-pdf texels), one-entry ranges (1xN / Nx1 maps), values on guide-cell edges, on
+    CDF entries and outside [0, 1); a non-monotone or NaN range gets no guide table (full search)."""
+    import numpy as np
+    rng = np.random.default_rng(5)
+    K = 64
+    edges = np.arange(K + 1, dtype=np.float32) / np.float32(K)
+    probes = np.concatenate([edges, np.nextafter(edges, np.float32(0)), np.nextafter(edges, np.float32(2)),
+                             rng.uniform(0, 1, 4000).astype(np.float32),
+                             np.float32([0.0, -0.0, 1.0, 0.9999999, 1.5, -0.25, 1e-30, np.nan])])
+    cases = []
+    for n in (1, 2, 3, 7, 64, 65, 513, 1024):
+        pdf = rng.exponential(1.0, n).astype(np.float32)
+        pdf[rng.uniform(size=n) < 0.3] = 0.0                     # plateaus
+        c = np.concatenate([[0.0], np.cumsum(pdf[:-1] / pdf.sum(), dtype=np.float32)]).astype(np.float32)
+        cases.append(("cdf%d" % n, c, True))
+    cases.append(("one-entry", np.float32([0.0]), True))
+    cases.append(("all-equal", np.full(9, 0.5, np.float32), True))
+    cases.append(("non-monotone", np.float32([0.0, 0.5, 0.4, 0.9]), False))
+    cases.append(("nan-row", np.float32([0.0, np.nan, 0.6, 0.9]), False))
+    cases.append(("nan-first", np.float32([np.nan, 0.2, 0.6]), False))
+    for name, v, want_guide in cases:
+        vals = np.concatenate([probes, v, np.nextafter(v, np.float32(-1)), np.nextafter(v, np.float32(2))])
+        built_guide, full, guided = _env_search(v, vals)
+        assert built_guide == want_guide, name
+        assert np.array_equal(full, guided), (name, np.nonzero(full != guided)[0][:8])

@@ -95,3 +95,31 @@ def test_bench_spawned_ranks_on_one_gpu(gpu, glass_scene, tmp_path):
     p.image_width, p.image_height, p.spp = 200, 120, 8
     ref = nart_amd.HipRenderer(glass_scene).render(p)
     assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
+    assert line["gather"].startswith("torch.distributed gather")
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_bench_one_process_multi_device(gpu, glass_scene, tmp_path, n):
+    """bench.py --one-process --gpus N: the path the C ABI ships (nart_hip_create_multi +
+    nart_hip_render_device: per-device threads, library gather to device 0, combine there).  On the
+    one-GPU box the N devices are GPU 0 repeated (device-copy gather); the line names the gather it
+    timed, and the combined image equals the single-device render bit for bit."""
+    import json
+    import subprocess
+    import nart_amd
+    out = str(tmp_path / "bench1p_img.npy")
+    env = dict(os.environ, NART_BENCH_SAME_DEVICE="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--one-process", "--gpus", str(n),
+                        "--size", "200x120x8", "--steps", "2", "--warmup", "1", "--dump-image", out],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == n and line["devices"] == [0] * n and line["image_finite"]
+    assert line["gather"].startswith("none" if n == 1 else "device-to-device copies")
+    img = np.load(out)
+    p = nart_amd.load_sessions(glass_scene.path)[0]
+    p.image_width, p.image_height, p.spp = 200, 120, 8
+    ref = nart_amd.HipRenderer(glass_scene).render(p)
+    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))

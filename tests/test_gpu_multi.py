@@ -72,13 +72,19 @@ def test_multi_device_rejects_bucket_api(gpu, glass_scene):
     assert e.value.code == -6  # NART_E_UNSUPPORTED: one context per rank for the bucket API
 
 
-def test_rccl_gather_failure_marks_context(gpu, glass_scene, monkeypatch):
-    """A gather that fails inside the RCCL group (test hook: a send to a rank that does not exist)
-    closes the group, returns NART_E_RCCL and leaves the context refusing further renders; a fresh
-    context then renders bit-identically (render.cpp:152-203 contract)."""
+@pytest.mark.parametrize("devices", [[0], [0, 1]])
+def test_rccl_gather_failure_marks_context(gpu, glass_scene, monkeypatch, devices):
+    """A gather that fails inside the RCCL group (test hook: the last device that owns buckets sends
+    to a rank that does not exist, after the other devices' receives are posted) closes the group,
+    returns NART_E_RCCL and leaves the context refusing further renders; a fresh context then
+    renders bit-identically (render.cpp:152-203 contract).  Two distinct devices need a node with
+    two GPUs (skipped on the one-GPU box)."""
+    import torch
+    if len(set(devices)) > torch.cuda.device_count():
+        pytest.skip("needs %d GPUs" % len(set(devices)))
     monkeypatch.setenv("NART_GATHER", "rccl")
     p = _params(glass_scene, 64, 48, 4)
-    m = nart_amd.HipRenderer(glass_scene, devices=[0])
+    m = nart_amd.HipRenderer(glass_scene, devices=devices)
     assert m.gather_mode() == "rccl"
     m.debug_fault(1)
     with pytest.raises(nart_amd.NartError) as e:
@@ -88,7 +94,7 @@ def test_rccl_gather_failure_marks_context(gpu, glass_scene, monkeypatch):
         m.render(p)
     assert e2.value.code == -5 and "destroy" in str(e2.value)
     m.close()
-    fresh = nart_amd.HipRenderer(glass_scene, devices=[0])
+    fresh = nart_amd.HipRenderer(glass_scene, devices=devices)
     assert _bits_equal(fresh.render(p), oracle.Oracle(glass_scene).render(p))
 
 

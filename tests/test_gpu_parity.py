@@ -225,9 +225,15 @@ def test_volume_queue_scheduler(gpu, volume_scenes, monkeypatch, kind, sparse, r
     monkeypatch.setenv("NART_VOL_SPARSE_F", "1.1")  # some groups of this small frame count as costly
     sc = volume_scenes[kind]
     p = _params(sc, 640, 360, 8)
-    g = nart_amd.HipRenderer(sc).render(p)
+    st = nart_amd.RenderStats()
+    g = nart_amd.HipRenderer(sc).render(p, st)
     r = oracle.Oracle(sc).render(p)
     assert _bits_equal(g, r), _report(g, r)
+    # the scheduler path under test really ran: the cost-probe queue always (more
+    # pixels than resident lanes), the sparse waves when asked for; nart_render_stats.schedule
+    names = st.schedule_names()
+    assert "vol_queue" in names, names
+    assert ("vol_sparse" in names) == (sparse != "64"), names
 
 
 def test_volume_per_sample(gpu, volume_scenes):
