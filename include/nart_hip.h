@@ -171,21 +171,20 @@ int nart_hip_bvh_info(const nart_scene_blob* scene, nart_bvh_info* out);
 int nart_hip_context_bvh(const nart_ctx* ctx, nart_bvh_info* out, double* build_ms);
 
 /* Kernel variant (all render bit-identical images):
-   0 = megakernel with a wave ray queue (default; one lane per pixel slot, the lanes of a wave
-       trace each other's queued shadow and continuation rays; scenes whose BVH stack does not fit
-       its 512-lane LDS layout run variant 3's kernel),
-   2 = megakernel with the traversal quorum on for every launch (parity tests at small sizes),
-   3 = megakernel, traversal quorum on when the launch spans >= 3 rounds of resident waves.
-   1 (the wavefront variant, 2x slower) was retired: NART_E_UNSUPPORTED. */
+   0 = megakernel with a wave ray queue (default; scenes whose BVH is too deep for its 512-lane
+       LDS layout run variant 3's kernel),
+   3 = megakernel, one lane per pixel, each query traced to completion.
+   1 (the wavefront variant, 2x slower) and 2 (variant 3 with a traversal quorum) were retired:
+   NART_E_UNSUPPORTED. */
 int nart_hip_set_variant(nart_ctx* ctx, int variant);
 
 /* Splat kernel (all bit-identical): -1 = automatic (the default: 4 when the launch fills >= 1
    wave per SIMD, else 3), 4 = skewed-time tile columns over the pixel-major sample layout (each
    sample fetched once per bucket), 3 = four tile pixels per lane over the sample-major layout;
-   2, 1, 0 = one tile pixel per lane with the compare-only / threshold / direct filter-index
-   arithmetic.  Modes fall back to a lower one where their preconditions (power-of-two buckets
-   <= 32, filter bounds 1-3, threshold table and weight LUT) do not hold.  (An LDS-staged mode
-   and an unskewed tile-column sweep measured slower and were retired.) */
+   1, 0 = one tile pixel per lane with the threshold / direct filter-index arithmetic (2 = 1).
+   Modes fall back to a lower one where their preconditions (power-of-two buckets <= 32, filter
+   bounds 1-3, threshold table and weight LUT) do not hold.  (An LDS-staged mode, an unskewed
+   tile-column sweep and a compare-only one-pixel mode measured slower and were retired.) */
 int nart_hip_set_splat_mode(nart_ctx* ctx, int mode);
 
 #ifdef __cplusplus

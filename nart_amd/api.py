@@ -351,9 +351,9 @@ class HipRenderer:
             self.set_splat_mode(splat_mode)
 
     def set_variant(self, variant):
-        """0 = megakernel with a wave ray queue (default), 2 / 3 = megakernel with the traversal
-        quorum always / by rounds of resident waves; identical results (1, the wavefront variant,
-        was retired)."""
+        """0 = megakernel with a wave ray queue (default), 3 = megakernel with one lane per pixel;
+        identical results (1, the wavefront variant, and 2, the traversal-quorum megakernel, were
+        retired)."""
         self._check(self._lib.nart_hip_set_variant(self._ctx, int(variant)))
 
     def set_splat_mode(self, mode):

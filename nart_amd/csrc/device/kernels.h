@@ -10,21 +10,30 @@
 namespace nd {
 
 // ---------------------------------------------------------------- nested-dielectric list
-// IntersectionInfo list (pathintegrator.h:9-19, pathintegrator.cpp:7-36, 123-142), kept in
-// registers: every access is an unrolled compare/select over MAXL slots (no dynamic indexing).
-template <int MAXL>
+// IntersectionInfo list (pathintegrator.h:9-19, pathintegrator.cpp:7-36, 123-142).  The first
+// ILIST_REG entries live in registers (every access an unrolled compare/select, no dynamic
+// indexing); a path can only grow the list by one entry per bounce, so renders with bounces <=
+// ILIST_REG never need more.  With EXT (bounces up to 32) entries ILIST_REG.. live in a per-lane
+// column of global memory, entry k at x[(k - ILIST_REG) * xs] as {id, eta bits}: deep nesting is
+// rare, so the kernels keep the register footprint of the short list and spill nothing (the
+// former 16- and 32-entry register lists spilled 50-97 VGPRs to scratch on every access).
+#define ILIST_REG 10
+#define ILIST_MAX 32
+// this lane's overflow column (formed at each use: no registers held across the kernel)
+#define ILIST_X(A) (EXT ? (A).ilist_ext + (blockIdx.x * blockDim.x + threadIdx.x) : nullptr)
+template <bool EXT>
 struct IList {
-    uint32_t id[MAXL];  // meshID (24 bit) | priority << 24
-    float eta[MAXL];
+    uint32_t id[ILIST_REG];  // meshID (24 bit) | priority << 24
+    float eta[ILIST_REG];
     uint32_t n;
 
-    ND bool valid(uint32_t meshID, uint32_t prio, float& eta_outer) const {
+    ND bool valid(uint32_t meshID, uint32_t prio, float& eta_outer, const uint2* x, uint32_t xs) const {
         eta_outer = 1.f;
         uint32_t lastId = 0;
         float lastEta = 1.f, penEta = 1.f;
         bool ok = true;
 #pragma unroll
-        for (int k = 0; k < MAXL; ++k) {
+        for (int k = 0; k < ILIST_REG; ++k) {
             if (k + 1 == (int)n) {
                 lastId = id[k] & 0xFFFFFFu;
                 lastEta = eta[k];
@@ -32,34 +41,60 @@ struct IList {
             if (k + 2 == (int)n) penEta = eta[k];
             if (k < (int)n && (prio & 0xFFu) < (id[k] >> 24)) ok = false;
         }
+        if (EXT && n > ILIST_REG) {
+            for (uint32_t k = ILIST_REG; k < n; ++k) {
+                const uint2 e = x[(size_t)(k - ILIST_REG) * xs];
+                if (k + 1 == n) {
+                    lastId = e.x & 0xFFFFFFu;
+                    lastEta = __uint_as_float(e.y);
+                }
+                if (k + 2 == n) penEta = __uint_as_float(e.y);
+                if ((prio & 0xFFu) < (e.x >> 24)) ok = false;
+            }
+        }
         if (n) {
             if (lastId != meshID) eta_outer = lastEta;
             else if (n >= 2) eta_outer = penEta;
         }
         return ok;
     }
-    ND void update(uint32_t meshID, uint32_t prio, float eta_s) {
+    ND void update(uint32_t meshID, uint32_t prio, float eta_s, uint2* x, uint32_t xs) {
         int found = -1;
 #pragma unroll
-        for (int k = 0; k < MAXL; ++k)
+        for (int k = 0; k < ILIST_REG; ++k)
             if (k < (int)n && (id[k] & 0xFFFFFFu) == meshID) found = k;  // most recent match
+        if (EXT && n > ILIST_REG)
+            for (uint32_t k = ILIST_REG; k < n; ++k)
+                if ((x[(size_t)(k - ILIST_REG) * xs].x & 0xFFFFFFu) == meshID) found = (int)k;
         if (found >= 0) {
+            // entries (found, n) move down by one
 #pragma unroll
-            for (int j = 0; j + 1 < MAXL; ++j) {
+            for (int j = 0; j + 1 < ILIST_REG; ++j) {
                 if (j >= found && j + 1 < (int)n) {
                     id[j] = id[j + 1];
                     eta[j] = eta[j + 1];
                 }
             }
+            if (EXT && n > ILIST_REG) {
+                if (found < ILIST_REG) {
+                    const uint2 e = x[0];
+                    id[ILIST_REG - 1] = e.x;
+                    eta[ILIST_REG - 1] = __uint_as_float(e.y);
+                }
+                for (uint32_t k = found > ILIST_REG ? (uint32_t)found : ILIST_REG; k + 1 < n; ++k)
+                    x[(size_t)(k - ILIST_REG) * xs] = x[(size_t)(k + 1 - ILIST_REG) * xs];
+            }
             --n;
         } else {
 #pragma unroll
-            for (int k = 0; k < MAXL; ++k) {
+            for (int k = 0; k < ILIST_REG; ++k) {
                 if (k == (int)n) {
                     id[k] = (meshID & 0xFFFFFFu) | ((prio & 0xFFu) << 24);
                     eta[k] = eta_s;
                 }
             }
+            if (EXT && n >= ILIST_REG)
+                x[(size_t)(n - ILIST_REG) * xs] = make_uint2((meshID & 0xFFFFFFu) | ((prio & 0xFFu) << 24), __float_as_uint(eta_s));
             ++n;
         }
     }
@@ -108,6 +143,9 @@ struct RenderArgs {
     // k_render_rq: queue entries with bit 31 set are priority pixels (the costliest of a small
     // shard): their rays are traced first and the traversal phase ends as soon as they resolve
     uint32_t rq_prio = 0;
+    // k_render_rq with rq_prio: also end a traversal phase once this many priority lanes have all
+    // their results while other priority rays are still in flight (0: only when all are resolved)
+    uint32_t rq_early = 0;
     // k_render_rq: entries with bit 30 set too are pixels dealt to two adjacent lanes, which run
     // the pixel's sample chain with RNG speculation (see k_render_rq); the queue then holds
     // qlen entries (the first round's pixels twice), not n_slots
@@ -121,6 +159,10 @@ struct RenderArgs {
     const uint32_t* gorder = nullptr;
     // k_primary: packet traversal (path.h traverse_packet) instead of one ray per lane
     uint32_t packet = 0;
+    // path kernels with bounces > ILIST_REG (EXT): the dielectric list's entries beyond
+    // ILIST_REG, [entry - ILIST_REG][lane], ilist_stride lanes (>= the launch's threads)
+    uint2* ilist_ext = nullptr;
+    uint32_t ilist_stride = 0;
 };
 #define RQ_PRIO_BIT 0x80000000u
 #define RQ_PAIR_BIT 0x40000000u
@@ -534,19 +576,11 @@ enum { ST_EXT = 0, ST_SH1 = 1, ST_SH2 = 2 };
 #define SECT(i, t) ((void)0)
 #endif
 #define NART_RENDER_LB __launch_bounds__(256, NART_RENDER_WAVES)
-#ifndef NART_QUORUM
-#define NART_QUORUM 8  // C3: 0 (lock step per query) 593 ms, 4: 530, 8: 517, 12: 518, 32: 595; -1: traverse() 569
-#endif
-#ifndef NART_QUORUM_ENV
-// environment-light scenes (more shading registers and work per hit): C4 1/8 shard -1: 645 ms,
-// 0: 668, 8: 701
-#define NART_QUORUM_ENV -1
-#endif
-// QR: traversal quorum on (throughput-bound launches: many rounds of resident waves) or off
-// (small shards, whose costliest pixels' serial chains set the time: the quorum lengthens them).
-template <int MAXL, bool COUNT, bool ENV, bool QR>
+// (Round 5: the traversal-quorum form of this kernel -- variant 2/3, C3 whole frame 517 vs 569 ms
+// before the ray-queue kernel replaced it -- was retired; k_render is the cost probe and the
+// fallback for BVHs too deep for the ray-queue kernel's LDS.)
+template <bool EXT, bool COUNT, bool ENV>
 __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
-    constexpr int QUORUM = QR ? (ENV ? NART_QUORUM_ENV : NART_QUORUM) : -1;
     // LDS traversal stack: stack_depth entries of (node code, entry distance) per lane,
     // laid out [depth][lane] so a wave's 64 lanes hit 64 distinct banks.
     extern __shared__ __attribute__((aligned(16))) int s_dyn[];
@@ -590,7 +624,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
     f3 L, beta, Le, c1, c2, betak, Led;
     float alpha = 0.f, eta_sampled = 1.f, eta_outer = 1.f, alphaTweak = 1.f;
     uint32_t flags = 0, bounce = 0;
-    IList<MAXL> list;
+    IList<EXT> list;
     list.n = 0;
     Ray ray, cur, nxt, sh2;
     float tmax = 0.f, sh2max = 0.f;
@@ -608,12 +642,8 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
     uint64_t sect[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const uint64_t sect_t0 = SECT_T();
 #endif
-    // Query in flight across loop iterations (traversal quorum, below).
-    Trav tq;
-    bool tracing = false;
     for (;;) {
         uint64_t st0 = SECT_T();
-        if (!tracing) {
         if (A.qhead) {
             // refill lanes whose pixel is done: one queue atomic per wave
             const bool need = new_sample && s >= A.spp;
@@ -687,39 +717,16 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
         }
         SECT(1, st0);
         st0 = SECT_T();
-        if constexpr (QUORUM >= 0) {
-            trav_begin(S, cur, tmax, stage != ST_EXT, tq);
-            tracing = S.geometry_visible;  // one-chunk scenes render no geometry (Q14)
-        }
-        }  // !tracing
 
         float bt;
         uint32_t bg;
         bool hit;
-        if constexpr (QUORUM >= 0) {
-        // Traversal with a quorum: lanes whose query resolves idle until at most QUORUM lanes
-        // of the wave are still tracing; then the resolved lanes shade and set up their next
-        // query while the rest keep their traversal state (tq) for the next iteration.  With 0
-        // every query of the wave resolves first (lock step per query).  Only the interleaving
-        // of lanes changes; each lane's operations are the same.
-        for (;;) {
-            if (tracing && trav_step<COUNT>(S, cur, tq, sc, stn, stride, cnt, s_nodes, nl)) tracing = false;
-            if (__popcll(__ballot(tracing)) <= QUORUM) break;
-        }
-        if (tracing) continue;
-        bt = tq.bestT;
-        bg = tq.bestG;
-        if (S.geometry_visible)
-            oc_resolve<COUNT>(S, cur, tq.tmax, tq.any, tq.risky, tq.bestInfo, fminf(tq.t2, oc_cull(S, tq.bestT)), bt,
-                              bg, cnt);
-        hit = bg != NO_HIT;
-        } else {
+        {
 #ifdef NART_WAVEPROF
         const uint64_t prof_t1 = __builtin_amdgcn_s_memtime();
         const uint32_t prof_n0 = cnt.nodes, prof_t0n = cnt.tris;
         ++prof_iters;
 #endif
-        tracing = false;
         hit = traverse<COUNT>(S, cur, tmax, stage != ST_EXT, bt, bg, sc, stn, stride, cnt, s_nodes, nl);
 #ifdef NART_WAVEPROF
         if (COUNT) {
@@ -736,7 +743,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
             if (stage == ST_EXT && hit) WPROF(cnt, 8);
         }
 #endif
-        }  // QUORUM
+        }
         SECT(2, st0);
         st0 = SECT_T();
         bool resolve = false;
@@ -756,7 +763,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
             BSDF bsdf;
             create_bsdf(S, is, alphaTweak, bsdf);
             use1 = use2 = false;
-            if (list.valid(is.meshID, is.priority, eta_outer)) {
+            if (list.valid(is.meshID, is.priority, eta_outer, ILIST_X(A), A.ilist_stride)) {
                 if (bounce == 0) alpha = 1.f;
                 const f3 wo = to_local(bsdf, neg(cur.d));
                 SECT(3, st0);
@@ -845,7 +852,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
                 have_ed = false;
             }
             if (cont) {
-                if (flags & F_TRANSMISSIVE) list.update(is.meshID, is.priority, eta_sampled);
+                if (flags & F_TRANSMISSIVE) list.update(is.meshID, is.priority, eta_sampled, ILIST_X(A), A.ilist_stride);
                 // Russian roulette (pathintegrator.cpp:236-246)
                 float q = gmax((beta.x + beta.y + beta.z) * 0.33333f, 0.f);
                 if (bounce > 3) {
@@ -1068,8 +1075,11 @@ NHD size_t rq_lds_bytes(uint32_t stack_depth, uint32_t block) {
 #ifndef NART_RQ_BLOCK
 #define NART_RQ_BLOCK 512
 #endif
-template <int MAXL, bool COUNT, bool ENV>
-__global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(DScene S, RenderArgs A) {
+// The counter pass (COUNT: untimed, its counts are per ray and do not depend on the schedule) runs
+// 256-lane blocks at one wave per SIMD, so its counters do not push the kernel past 256 VGPRs.
+#define RQ_BLOCK_OF(COUNT) ((COUNT) ? 256 : NART_RQ_BLOCK)
+template <bool EXT, bool COUNT, bool ENV>
+__global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) void k_render_rq(DScene S, RenderArgs A) {
     extern __shared__ __attribute__((aligned(16))) int s_dyn[];
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6;
@@ -1154,7 +1164,7 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
     f3 c1 = F3(0.f, 0.f, 0.f), c2 = F3(0.f, 0.f, 0.f), betak = F3(0.f, 0.f, 0.f);
     float alpha = 0.f, eta_sampled = 1.f, eta_outer = 1.f, alphaTweak = 1.f;
     uint32_t flags = 0, bounce = 0;
-    IList<MAXL> list;
+    IList<EXT> list;
     list.n = 0;
     bool lightHit = false, use1 = false, use2 = false, have_ed = false, ext_pending = false;
     bool waiting = false;  // rays of this lane's path are queued or in flight
@@ -1482,11 +1492,11 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
             uint32_t gprim = NO_HIT;
             {
                 const uint64_t si = soff + (uint64_t)s * sstr;
-                // (not in the environment-light build, whose registers are already spilling)
-                if (!ENV && s == c_s) {
+                // (not in the environment-light, deep-list or counter-pass builds, whose registers would spill)
+                if (!ENV && !EXT && !COUNT && s == c_s) {
                     sm = c_sm;
                     gprim = c_prim;
-                } else if (!ENV && sstr == 1u && (si & 1u) == 0u && s + 1u < A.spp) {
+                } else if (!ENV && !EXT && !COUNT && sstr == 1u && (si & 1u) == 0u && s + 1u < A.spp) {
                     const float4 q = reinterpret_cast<const float4*>(A.samples)[si >> 1];
                     sm = make_float2(q.x, q.y);
                     c_sm = make_float2(q.z, q.w);
@@ -1556,7 +1566,7 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
             use1 = use2 = false;
             bool cont;
             f3 no, nd;
-            if (list.valid(is.meshID, is.priority, eta_outer)) {
+            if (list.valid(is.meshID, is.priority, eta_outer, ILIST_X(A), A.ilist_stride)) {
                 if (bounce == 0) alpha = 1.f;
                 const f3 wo = to_local(bsdf, neg(cur.d));
                 // ---- EstimateDirect (pathintegrator.cpp:38-121)
@@ -1638,7 +1648,7 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
                 have_ed = false;
             }
             if (cont) {
-                if (flags & F_TRANSMISSIVE) list.update(is.meshID, is.priority, eta_sampled);
+                if (flags & F_TRANSMISSIVE) list.update(is.meshID, is.priority, eta_sampled, ILIST_X(A), A.ilist_stride);
                 // Russian roulette (pathintegrator.cpp:236-246)
                 float q = gmax((beta.x + beta.y + beta.z) * 0.33333f, 0.f);
                 if (bounce > 3) {
@@ -1764,6 +1774,14 @@ __global__ __launch_bounds__(NART_RQ_BLOCK, NART_RENDER_WAVES) void k_render_rq(
 #endif
             // priority rays all resolved and a priority lane waits on its results: shade it now
             if (A.rq_prio && ph == pt && __ballot(tracing && tr_prio) == 0 && __ballot(waiting && prio) != 0) break;
+            if (A.rq_early) {
+                bool ready = false;
+                if (waiting && prio) {
+                    const uint4 r = *my_res;
+                    ready = (!ext_pending || r.x != RQ_PENDING) && (!use1 || r.y != 2u) && (!use2 || r.z != 2u);
+                }
+                if ((uint32_t)__popcll(__ballot(ready)) >= A.rq_early) break;
+            }
             if (ph == pt && nh == nt && (uint32_t)__popcll(__ballot(tracing)) <= A.rq_quorum) break;
         }
 #ifdef NART_WAVEPROF
@@ -1872,38 +1890,18 @@ ND bool splat_hits_thr(const SplatArgs& A, const float* table, const float* thr,
     return hit;
 }
 
-// Per-lane constants of splat_hits_fast: the tile pixel in image coordinates for a sample of the
-// lane's own bucket column / row (xsA, ysA) and of the next one (xsB, ysB), and the coordinate
-// from which a sample counts as the next bucket's (edge = bucket origin + B + fb).
-struct SplatLane {
-    float xsA, xsB, ysA, ysB, edgeX, edgeY;
-};
-
-// splat_hits_thr for a power-of-two bucket size, with the per-pair work cut to compares:
+// splat_hits_fast: the compare-only form of splat_hits_thr for a power-of-two bucket size, which
+// k_splat_col4 and k_splat_skew inline (the one-pixel-per-lane kernel that used it alone, splat
+// mode 2, was retired in round 5):
 //  * k = floor((sc - fb) / B): sc - fb is exact (both are multiples of ulp(sc)) and lies in
 //    [origin + S, origin + S + 1] for bucket-local column S, and / B is exact, so k is the bucket
-//    column, plus one exactly when sc - fb >= origin + B, i.e. sc >= edge;
+//    column, plus one exactly when sc - fb >= origin + B, i.e. sc >= edge (= bucket origin + B + fb);
 //  * floor(a) <= xs  <=>  a < xs + 1  and  xs < ceil(b)  <=>  xs < b  for an integer xs, with
 //    a = RN(sc - fw) and b = RN(sc + fw) as the reference rounds them;
 //  * dist and the filter index as in splat_hits_thr.
-ND bool splat_hits_fast(const SplatArgs& A, const SplatLane& P, const float* table, const float* thr, float scx,
-                        float scy, float& w) {
-    const float xs = scx >= P.edgeX ? P.xsB : P.xsA;
-    const float ys = scy >= P.edgeY ? P.ysB : P.ysA;
-    const bool hit = (scx - A.fw) < xs + 1.f && xs < (scx + A.fw) && (scy - A.fw) < ys + 1.f && ys < (scy + A.fw);
-    const float distX = (xs + 0.5f) - scx;
-    const float distY = (ys + 0.5f) - scy;
-    const float d2 = distX * distX + distY * distY;
-    int g = (int)(__builtin_amdgcn_sqrtf(d2) * A.idx_scale);
-    g = g < 0 ? 0 : (g > 63 ? 63 : g);
-    const float t0 = thr[g], t1 = thr[g + 1];
-    const int fi = g - (d2 < t0 ? 1 : 0) + (d2 >= t1 ? 1 : 0);
-    w = table[fi];
-    return hit;
-}
 
 // MODE 0: direct AddSample arithmetic (splat_hits); 1: filter index from thresholds
-// (splat_hits_thr); 2: thresholds and a power-of-two bucket size (splat_hits_fast).
+// (splat_hits_thr).  The fallbacks of the splat: any bucket size and filter width.
 template <int MODE>
 __global__ __launch_bounds__(256) void k_splat(SplatArgs A) {
     __shared__ float s_table[64];
@@ -1912,9 +1910,7 @@ __global__ __launch_bounds__(256) void k_splat(SplatArgs A) {
     if (MODE > 0 && threadIdx.x < 65) s_thr[threadIdx.x] = A.thr[threadIdx.x];
     __syncthreads();
 #define NART_SPLAT_HITS(scx, scy, w)                                                                        \
-    (MODE == 2   ? splat_hits_fast(A, P, s_table, s_thr, scx, scy, w)                                      \
-     : MODE == 1 ? splat_hits_thr(A, s_table, s_thr, scx, scy, tx, ty, w)                                  \
-                 : splat_hits(A, s_table, scx, scy, tx, ty, w))
+    (MODE == 1 ? splat_hits_thr(A, s_table, s_thr, scx, scy, tx, ty, w) : splat_hits(A, s_table, scx, scy, tx, ty, w))
     const uint32_t tpx = A.tile * A.tile;
     const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (uint64_t)A.n_buckets * tpx) return;
@@ -1927,13 +1923,6 @@ __global__ __launch_bounds__(256) void k_splat(SplatArgs A) {
     const int bw = (int)(x1 - x0), bh = (int)(y1 - y0);
     const uint32_t npx = (uint32_t)(bw * bh);
     const uint32_t base = A.bucket_base[bi];
-    SplatLane P;
-    P.xsA = (float)(tx + x0);
-    P.xsB = (float)(tx + x0 + A.B);
-    P.ysA = (float)(ty + y0);
-    P.ysB = (float)(ty + y0 + A.B);
-    P.edgeX = (float)(x0 + A.B + A.fb);
-    P.edgeY = (float)(y0 + A.B + A.fb);
     // Candidate source pixels.  A sample of bucket-local column S has sc - x0 in [S+fb, S+fb+1],
     // so its splat columns span [S+fb-ceil(fw), S+fb+1+fw): tile column tx can only be reached
     // from S in [tx-fb-ceil(fw), tx-fb+ceil(fw)].  Samples of the last column can also wrap to

@@ -167,120 +167,15 @@ ND bool maj_next(const DMedium& m, MajIter& it, float& sigma, float& t0, float& 
     return true;
 }
 
-// VolumeIntegrator::Li_alpha with SampleT_maj inlined (T_maj only feeds an unused callback
-// argument, so its exp() factors are not evaluated).
-ND f4 li_volume(const DScene& S, const RenderArgs& A, uint32_t& rng, f3 o, f3 d, uint32_t& work) {
-    const DMedium& m = S.medium;
-    f3 L = F3(0.f, 0.f, 0.f);
-    const f3 beta = F3(1.f, 1.f, 1.f);
-    uint32_t bounce = 0;
-    for (;;) {
-        bool scattered = false, terminated = false;
-        (void)rng_float(rng);  // u: passed to SampleT_maj, unused there
-        float uMode = rng_float(rng);
-        MajIter it;
-        if (m.present && medium_sample_ray(m, o, d, it)) {
-            const f3 ro = o, rd = d;  // SampleT_maj's copy of the ray
-            bool done = false;
-            while (!done) {
-                float sigma, t0, t1;
-                if (!maj_next(m, it, sigma, t0, t1)) break;
-                float tMin = t0;
-                for (;;) {
-                    ++work;  // tentative collisions: the cost probe's measure
-                    const float t = tMin + (-glibc_logf(1.f - rng_float(rng)) / sigma);
-                    if (!(t < t1)) break;
-                    const f3 p = add(ro, muls(rd, t));
-                    if (p.x < m.bmin[0] || p.y < m.bmin[1] || p.z < m.bmin[2] || p.x > m.bmax[0] || p.y > m.bmax[1] ||
-                        p.z > m.bmax[2]) {
-                        done = true;
-                        break;
-                    }
-                    const f3 bmin = F3(m.bmin[0], m.bmin[1], m.bmin[2]);
-                    const f3 bs = sub(F3(m.bmax[0], m.bmax[1], m.bmax[2]), bmin);
-                    const f3 q0 = sub(p, bmin);
-                    const float density = dg_lookup(m, m.density, F3(q0.x / bs.x, q0.y / bs.y, q0.z / bs.z));
-                    const float sa = m.sigma_a * density, ss = m.sigma_s * density;
-                    const float pAbsorb = sa / sigma;
-                    const float pScatter = ss / sigma;
-                    if (uMode < pAbsorb) {
-                        terminated = true;
-                        L = add(L, mul(muls(F3(m.Le[0], m.Le[1], m.Le[2]), density), beta));
-                        done = true;
-                        break;
-                    } else if (uMode < pAbsorb + pScatter) {
-                        if (bounce++ > A.bounces) {
-                            terminated = true;
-                            done = true;
-                            break;
-                        }
-                        const float a = rng_float(rng);
-                        const float b = rng_float(rng);
-                        o = p;
-                        d = uniform_sample_sphere(F2(a, b));
-                        scattered = true;
-                        done = true;
-                        break;
-                    }
-                    uMode = rng_float(rng);  // null collision
-                    tMin = t;
-                }
-            }
-        }
-        if (terminated) break;
-        if (scattered) continue;
-        float lightTMax = __builtin_inff();
-        f3 Le = F3(0.f, 0.f, 0.f);
-        for (uint32_t j = 0; j < S.num_lights; ++j) {
-            float lt = __builtin_inff();
-            const f3 Li = light_li(S, S.lights[j], o, d, nullptr, lt);
-            if (lt < lightTMax) {
-                Le = Li;
-                lightTMax = lt;
-            }
-        }
-        L = add(L, mul(Le, beta));
-        break;
-    }
-    return F4(L.x, L.y, L.z, 1.f);
-}
-
-// One lane per traced pixel.  With A.queue the launch order of pixels is the queue's (the
-// scheduler puts the costliest wave-sized groups first, render.hip dispatch_volume); with
-// A.cost the kernel is the cost probe (tentative collisions of the pixel's first samples).
-template <bool COUNT>
-__global__ __launch_bounds__(256) void k_render_volume(DScene S, RenderArgs A) {
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= A.n_slots) return;
-    const uint32_t slot = A.queue ? A.queue[gid] : gid;
-    const uint32_t xy = A.slot_xy[slot];
-    const uint32_t px = xy & 0xFFFFu, py = xy >> 16;
-    uint32_t rng = A.rng0[slot];
-    const SlotSO so = A.slot_so[slot];
-    const float2* smp = A.samples + so.first;
-    float4* out = A.Lout + so.first;
-    uint32_t work = 0;
-    for (uint32_t s = 0; s < A.spp; ++s) {
-        const float2 sm = smp[(size_t)s * so.stride];
-        const Ray r = cast_ray(S, F2(sm.x, sm.y), A.W, A.H, px, py);
-        const f4 L = li_volume(S, A, rng, r.o, r.d, work);
-        out[(size_t)s * so.stride] = make_float4(L.x, L.y, L.z, L.w);
-    }
-    if (A.cost) {
-        A.cost[gid] = work + A.spp;
-        return;
-    }
-    if (COUNT) atomicAdd(&A.counters[0], (unsigned long long)A.spp);
-}
-
-// The same computation as a per-lane state machine (the default).  k_render_volume runs li_volume
-// to completion for every sample, so a wave waits for its slowest lane at every sample and costs
-// sum_s max_lane(collisions); the number of collisions per sample is roughly geometric, so that is
-// several times the mean.  Here one loop iteration advances every lane by one tentative collision
-// (plus whatever cheap steps lead up to it: a new sample, a new ray segment, the next majorant
-// segment), and a lane whose sample ends starts its next sample at once, so the wave costs about
-// max_lane sum_s(collisions).  Each lane performs exactly the RNG draws and float operations of
-// li_volume in the same order: the output is bit-identical.
+// VolumeIntegrator::Li_alpha (volumeintegrator.cpp:3-84) with SampleT_maj (media.h:128-181)
+// inlined -- T_maj only feeds an unused callback argument, so its exp() factors are not evaluated
+// -- as a per-lane state machine.  Running each sample to completion (the round-1 kernel, retired
+// in round 5) made a wave wait for its slowest lane at every sample: sum_s max_lane(collisions),
+// several times the mean for the roughly geometric collision counts.  Here one loop iteration
+// advances every lane by one tentative collision (plus whatever cheap steps lead up to it: a new
+// sample, a new ray segment, the next majorant segment), and a lane whose sample ends starts its
+// next sample at once, so the wave costs about max_lane sum_s(collisions).  Each lane performs
+// exactly the reference's RNG draws and float operations in its order: bit-identical.
 // WV: minimum waves per SIMD requested from the register allocator (dispatch_volume: 4 on
 // throughput-bound launches, 1 on small shards)
 template <bool COUNT, int WV>

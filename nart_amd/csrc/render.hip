@@ -74,6 +74,8 @@ struct nart_ctx {
     // megakernel work queue (launch_render)
     uint32_t* d_queue = nullptr;
     uint32_t* d_cost = nullptr;
+    void* d_ilist = nullptr;   // dielectric-list columns beyond ILIST_REG (bounces > ILIST_REG)
+    size_t cap_ilist = 0;
     uint32_t* d_keys[2] = {nullptr, nullptr};
     uint32_t* d_vals[2] = {nullptr, nullptr};
     uint32_t* d_qhead = nullptr;
@@ -604,21 +606,36 @@ int sort_groups_by_cost(nart_ctx* ctx, uint32_t n, uint32_t* out, hipStream_t st
     return NART_OK;
 }
 
-template <int MAXL, bool COUNT, bool ENV>
-int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
-    auto kern = k_render<MAXL, COUNT, ENV, false>;
-    auto kern_q = k_render<MAXL, COUNT, ENV, true>;
-    auto kern_rq = k_render_rq<MAXL, COUNT, ENV>;
+template <bool EXT, bool COUNT, bool ENV>
+int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
+    auto kern = k_render<EXT, COUNT, ENV>;
+    auto kern_rq = k_render_rq<EXT, COUNT, ENV>;
+    constexpr uint32_t RQB = RQ_BLOCK_OF(COUNT);  // ray-queue block (kernels.h)
+    RenderArgs a = a_in;
+    if (EXT) {
+        // the dielectric list's entries beyond ILIST_REG: one column per thread of the largest
+        // launch below (whole 512-thread blocks over every slot)
+        const size_t lanes = ((size_t)a.n_slots + 511) / 512 * 512;
+        const size_t bytes = lanes * (ILIST_MAX - ILIST_REG) * sizeof(uint2);
+        if (bytes > ctx->cap_ilist) {
+            if (ctx->d_ilist) HIPCHK(hipFree(ctx->d_ilist));
+            ctx->d_ilist = nullptr;
+            ctx->cap_ilist = 0;
+            if (hipMalloc(&ctx->d_ilist, bytes) != hipSuccess) return fail(ctx, NART_E_OOM, "hipMalloc dielectric lists");
+            ctx->cap_ilist = bytes;
+        }
+        a.ilist_ext = static_cast<uint2*>(ctx->d_ilist);
+        a.ilist_stride = (uint32_t)lanes;
+    }
     static std::atomic<uint64_t> attr{0};  // dynamic LDS above the 64 KiB default, set once per device
     const uint64_t dbit = 1ull << (ctx->device & 63);
     if (!(attr.load() & dbit)) {
-        for (const void* f : {(const void*)kern, (const void*)kern_q, (const void*)k_render<MAXL, true, ENV, false>,
+        for (const void* f : {(const void*)kern, (const void*)k_render<EXT, true, ENV>,
                               (const void*)kern_rq, (const void*)k_primary<COUNT, ENV>})
             hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr.fetch_or(dbit);
     }
-    // variant 0: ray-queue kernel; 2: k_render with the traversal quorum on every launch;
-    // 3: k_render with the quorum chosen by rounds of resident waves (the previous default).
+    // variant 0: ray-queue kernel; 3: k_render (one lane per pixel, the fallback below).
     // The ray-queue kernel's 512-lane blocks keep a stack_depth * 4 KiB traversal stack plus
     // 60 KiB of ray outboxes in LDS: a BVH deeper than 24 levels does not fit, and those scenes
     // run k_render (256-lane blocks, stack_depth * 2 KiB) instead -- same image.
@@ -626,11 +643,9 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     // camera rays first, coherently (k_primary); NART_PRIMARY=0 leaves them to the path kernel
     const bool primary = !std::getenv("NART_PRIMARY") || std::atoi(std::getenv("NART_PRIMARY")) != 0;
 
-    // NART_QUORUM_MIN_ROUNDS: rounds of resident waves from which the quorum kernel is used (C3:
-    // whole frame 16 rounds 569 -> 517 ms with it, 1/2 frame 8 rounds 332 -> 301, 1/4 4 rounds
-    // 183 -> 179, 1/8 2 rounds 108 -> 134)
-    const double q_rounds =
-        std::getenv("NART_QUORUM_MIN_ROUNDS") ? std::atof(std::getenv("NART_QUORUM_MIN_ROUNDS")) : 3.0;
+    // rounds of resident waves from which a launch counts as throughput-bound: ray-queue quorum 8
+    // (else 0), no priority lanes or speculative pairs
+    const double q_rounds = 3.0;
     RenderArgs b = a;
     b.lds_nodes = render_lds_nodes(ctx);
     const size_t lds = (size_t)ctx->stack_depth * 256 * 8 + (size_t)b.lds_nodes * sizeof(BVHNode);
@@ -653,8 +668,8 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
         ctx->sched |= NART_SCHED_PRIMARY;
         brq.prim = ctx->d_prim;
     }
-    brq.lds_nodes = render_lds_nodes(ctx, rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK), NART_RQ_BLOCK / 256);
-    const size_t lds_rq = rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK) + (size_t)brq.lds_nodes * sizeof(BVHNode);
+    brq.lds_nodes = render_lds_nodes(ctx, rq_lds_bytes(ctx->stack_depth, RQB), RQB / 256);
+    const size_t lds_rq = rq_lds_bytes(ctx->stack_depth, RQB) + (size_t)brq.lds_nodes * sizeof(BVHNode);
     const dim3 block(256);
     uint32_t blocks = (a.n_slots + 255) / 256;
     const int mode = queue_mode();
@@ -664,7 +679,6 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     const uint32_t resident = (uint32_t)std::max(1, cus * std::max(per_cu, 1));
     const uint32_t W = resident * 4;  // resident (persistent) waves
     const double R = (double)a.n_slots / (64.0 * W);  // rounds of resident waves
-    if (ctx->variant == 2 || R >= q_rounds) kern = kern_q;
     // the ray-queue kernel takes kern's place (its own LDS layout); the cost probe keeps k_render
     auto launch = [&](uint32_t nblocks, const RenderArgs& args) {
         if (rq) {
@@ -676,8 +690,8 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             r2.lds_nodes = brq.lds_nodes;
             r2.prim = brq.prim;
             r2.rq_quorum = rqq >= 0 ? (uint32_t)rqq : (R >= q_rounds ? 8u : 0u);
-            const uint32_t per = NART_RQ_BLOCK / 256;  // launches are counted in blocks of 256
-            hipLaunchKernelGGL(kern_rq, dim3((nblocks + per - 1) / per), dim3(NART_RQ_BLOCK), lds_rq, st, ctx->scene, r2);
+            const uint32_t per = RQB / 256;  // launches are counted in blocks of 256
+            hipLaunchKernelGGL(kern_rq, dim3((nblocks + per - 1) / per), dim3(RQB), lds_rq, st, ctx->scene, r2);
         } else {
             hipLaunchKernelGGL(kern, dim3(nblocks), block, lds, st, ctx->scene, args);
         }
@@ -706,7 +720,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                 const bool groups = rq && (!std::getenv("NART_RQ_GROUPS") || std::atoi(std::getenv("NART_RQ_GROUPS")) != 0);
                 if (groups) {
                     int per_cu_rq = 0;
-                    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_rq, (const void*)kern_rq, NART_RQ_BLOCK,
+                    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_rq, (const void*)kern_rq, RQB,
                                                                        lds_rq));
                     HIPCHK(hipMemsetAsync(ctx->d_qhead, 0, sizeof(uint32_t), st));
                     b.ghead = ctx->d_qhead;
@@ -723,7 +737,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                         pb.spp = 1;
                         pb.cost = ctx->d_cost;
                         pb.ghead = nullptr;
-                        hipLaunchKernelGGL((k_render<MAXL, true, ENV, false>), dim3(blocks), block, lds, st, ctx->scene, pb);
+                        hipLaunchKernelGGL((k_render<EXT, true, ENV>), dim3(blocks), block, lds, st, ctx->scene, pb);
                         const uint32_t ng = (n + 63) / 64;
                         const dim3 gg((ng + 255) / 256);
                         hipLaunchKernelGGL(k_group_keys, gg, block, 0, st, ctx->d_cost, n, ctx->d_keys[0], ctx->d_vals[0]);
@@ -744,7 +758,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                         }
                     }
                     // launches are counted in blocks of 256 threads
-                    blocks = std::min(blocks, (uint32_t)std::max(1, cus * std::max(per_cu_rq, 1)) * (NART_RQ_BLOCK / 256));
+                    blocks = std::min(blocks, (uint32_t)std::max(1, cus * std::max(per_cu_rq, 1)) * (RQB / 256));
                 }
                 launch(blocks, b);
                 HIPCHK(hipGetLastError());
@@ -758,7 +772,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                 RenderArgs pb = b;  // cost probe: the first sample of every pixel
                 pb.spp = 1;
                 pb.cost = ctx->d_cost;
-                hipLaunchKernelGGL((k_render<MAXL, true, ENV, false>), dim3(blocks), block, lds, st, ctx->scene, pb);
+                hipLaunchKernelGGL((k_render<EXT, true, ENV>), dim3(blocks), block, lds, st, ctx->scene, pb);
                 int rc2 = sort_groups_by_cost(ctx, n, k == 64u ? ctx->d_queue : ctx->d_cost, st);
                 if (rc2) return rc2;
                 size_t tmp = 0;
@@ -793,6 +807,8 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                                    n, W, k, pbit, pairs, ctx->d_queue);
                 b.rq_prio = pbit ? 1u : 0u;
                 b.rq_pairs = pairs;
+                // NART_RQ_EARLY (A/B): end a traversal phase once that many priority lanes are ready
+                b.rq_early = pbit && std::getenv("NART_RQ_EARLY") ? (uint32_t)std::max(0, std::atoi(std::getenv("NART_RQ_EARLY"))) : 0u;
                 b.qlen = qlen;
                 if (pbit) ctx->sched |= NART_SCHED_PRIORITY;
                 if (pairs) ctx->sched |= NART_SCHED_SPEC_PAIRS;
@@ -803,7 +819,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
                 b.qhead = ctx->d_qhead;
                 ctx->sched |= NART_SCHED_PROBE_QUEUE;
                 // whole ray-queue blocks, so that every first-round lane's entry lies below qbase
-                const uint32_t per = rq ? NART_RQ_BLOCK / 256 : 1u;
+                const uint32_t per = rq ? RQB / 256 : 1u;
                 blocks = (resident + per - 1u) / per * per;
                 b.qbase = blocks * 256;
             }
@@ -816,10 +832,12 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
 
 template <bool ENV>
 int launch_render_maxl(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
+    // a path grows the dielectric list by at most one entry per bounce: the register list alone
+    // serves bounces <= ILIST_REG; deeper ones (up to 32) spill it to the per-lane columns
     const bool c = ctx->counters;
-    if (a.bounces <= 10) return c ? launch_render<10, true, ENV>(ctx, a, st) : launch_render<10, false, ENV>(ctx, a, st);
-    if (a.bounces <= 16) return c ? launch_render<16, true, ENV>(ctx, a, st) : launch_render<16, false, ENV>(ctx, a, st);
-    return c ? launch_render<32, true, ENV>(ctx, a, st) : launch_render<32, false, ENV>(ctx, a, st);
+    if (a.bounces <= ILIST_REG)
+        return c ? launch_render<false, true, ENV>(ctx, a, st) : launch_render<false, false, ENV>(ctx, a, st);
+    return c ? launch_render<true, true, ENV>(ctx, a, st) : launch_render<true, false, ENV>(ctx, a, st);
 }
 
 int dispatch_megakernel(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
@@ -833,13 +851,11 @@ int dispatch_megakernel(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
 int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     const dim3 block(256);
     const uint32_t blocks = (a.n_slots + 255) / 256;
-    // NART_VOL_SM=0: the per-sample lock-step kernel (A/B timing only; same output)
-    const bool sm = !(std::getenv("NART_VOL_SM") && std::getenv("NART_VOL_SM")[0] == '0');
     RenderArgs b = a;
     // small density grids (C5: 2x2x2) are read from LDS (NART_VOL_LDS=0: from global memory)
     const bool vol_lds = !(std::getenv("NART_VOL_LDS") && std::getenv("NART_VOL_LDS")[0] == '0');
     const uint32_t nd = ctx->scene.medium.present ? ctx->scene.medium.rx * ctx->scene.medium.ry * ctx->scene.medium.rz : 0;
-    b.lds_nodes = (sm && vol_lds && nd <= 4096u) ? nd : 0u;
+    b.lds_nodes = (vol_lds && nd <= 4096u) ? nd : 0u;
     const size_t dl = (size_t)b.lds_nodes * sizeof(float);
     // occupancy: launches of >= 8 rounds of resident waves use the 4-waves-per-SIMD build (C5 frame,
     // 10.5 rounds: 134 -> 122 ms); smaller ones keep the unconstrained build, whose lanes' serial
@@ -861,8 +877,7 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             RenderArgs pb = b;
             pb.spp = 4;
             pb.cost = ctx->d_cost;
-            if (sm) hipLaunchKernelGGL((k_render_volume_sm<false, 1>), dim3(blocks), block, dl, st, ctx->scene, pb);
-            else hipLaunchKernelGGL((k_render_volume<false>), dim3(blocks), block, 0, st, ctx->scene, pb);
+            hipLaunchKernelGGL((k_render_volume_sm<false, 1>), dim3(blocks), block, dl, st, ctx->scene, pb);
             rc = sort_groups_by_cost(ctx, n, ctx->d_queue, st);
             if (rc) return rc;
             b.queue = ctx->d_queue;
@@ -880,7 +895,7 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             const char* re = std::getenv("NART_VOL_SPARSE_ROUNDS");
             const uint32_t S = se ? std::max(1u, std::min(64u, (uint32_t)std::atoi(se))) : 16u;
             const double f = fe ? std::atof(fe) : 4.0, max_rounds = re ? std::atof(re) : 2.0;
-            if (sm && S < 64u && (64u % S) == 0u && (double)blocks / (double)resident < max_rounds) {
+            if (S < 64u && (64u % S) == 0u && (double)blocks / (double)resident < max_rounds) {
                 const uint32_t ng = (n + 63) / 64;
                 std::vector<uint32_t> keys(ng);
                 HIPCHK(hipMemcpyAsync(keys.data(), ctx->d_keys[1], (size_t)ng * 4, hipMemcpyDeviceToHost, st));
@@ -906,14 +921,9 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             HIPCHK(hipGetLastError());
         }
     }
-    if (sm) {
-        if (ctx->counters) hipLaunchKernelGGL((k_render_volume_sm<true, 1>), dim3(grid), block, dl, st, ctx->scene, b);
-        else if (w4) hipLaunchKernelGGL((k_render_volume_sm<false, 4>), dim3(grid), block, dl, st, ctx->scene, b);
-        else hipLaunchKernelGGL((k_render_volume_sm<false, 1>), dim3(grid), block, dl, st, ctx->scene, b);
-    } else {
-        if (ctx->counters) hipLaunchKernelGGL((k_render_volume<true>), dim3(blocks), block, 0, st, ctx->scene, b);
-        else hipLaunchKernelGGL((k_render_volume<false>), dim3(blocks), block, 0, st, ctx->scene, b);
-    }
+    if (ctx->counters) hipLaunchKernelGGL((k_render_volume_sm<true, 1>), dim3(grid), block, dl, st, ctx->scene, b);
+    else if (w4) hipLaunchKernelGGL((k_render_volume_sm<false, 4>), dim3(grid), block, dl, st, ctx->scene, b);
+    else hipLaunchKernelGGL((k_render_volume_sm<false, 1>), dim3(grid), block, dl, st, ctx->scene, b);
     HIPCHK(hipGetLastError());
     return NART_OK;
 }
@@ -1253,8 +1263,9 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
 #define NART_SPLAT_NP 4
 #endif
         const uint64_t n4 = (uint64_t)nbk * g.tile_size * ((g.tile_size + NART_SPLAT_NP - 1) / NART_SPLAT_NP);
-        // splat modes (all bit-identical, mode 3 the default): 3 four tile pixels per lane; 2 / 1 / 0
-        // one tile pixel per lane with the compare-only / threshold / direct filter-index arithmetic
+        // splat modes (all bit-identical): 4 skewed time, 3 four tile pixels per lane (power-of-two
+        // buckets); 1 / 0 one tile pixel per lane with the threshold / direct filter-index arithmetic
+        // (any bucket size; 2 selects 1 since the compare-only one-pixel kernel was retired)
         if (skew) {
             ctx->sched |= NART_SCHED_SPLAT_SKEW;
             const uint32_t nb = skew_bands;  // tile-row bands per bucket (k_splat_skew's NB)
@@ -1276,7 +1287,6 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
                 hipLaunchKernelGGL((k_splat_col4<NART_SPLAT_NP, false>), dim3((uint32_t)((n4 + 255) / 256)), dim3(256),
                                    0, st, sa);
         }
-        else if (sa.thr && sa.invB != 0.f && splat_mode >= 2) hipLaunchKernelGGL(k_splat<2>, sg, dim3(256), 0, st, sa);
         else if (sa.thr && splat_mode >= 1) hipLaunchKernelGGL(k_splat<1>, sg, dim3(256), 0, st, sa);
         else hipLaunchKernelGGL(k_splat<0>, sg, dim3(256), 0, st, sa);
         HIPCHK(hipGetLastError());
@@ -1521,7 +1531,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     ctx->device = device_id;
     if (const char* v = std::getenv("NART_VARIANT")) {
         const int var = std::atoi(v);
-        if (var == 0 || var == 2 || var == 3) ctx->variant = var;
+        if (var == 0 || var == 3) ctx->variant = var;
     }
     if (const char* v = std::getenv("NART_SPLAT_MODE")) ctx->splat_mode = std::max(-1, std::min(4, std::atoi(v)));
     int ndev = 0;
@@ -1739,7 +1749,7 @@ void nart_hip_destroy(nart_ctx* ctx) {
                     ctx->d_L, ctx->d_bucket_ids, ctx->d_bucket_base, ctx->d_table, ctx->d_lut, ctx->d_counters, ctx->d_envs, ctx->d_density,
                     ctx->d_oc_nodes, ctx->d_oc_chunks, ctx->d_oc_tris, ctx->d_tri_leaf, ctx->d_oc_lock, ctx->d_oc_heap,
                     ctx->d_queue, ctx->d_cost, ctx->d_keys[0], ctx->d_keys[1], ctx->d_vals[0], ctx->d_vals[1],
-                    ctx->d_qhead, ctx->d_sort_tmp};
+                    ctx->d_qhead, ctx->d_sort_tmp, ctx->d_ilist};
     for (void* b : bufs)
         if (b) hipFree(b);
     for (void* b : {ctx->d_gather, ctx->d_image})  // nart_hip_render_device's tiles and image
@@ -1775,10 +1785,10 @@ int nart_hip_set_variant(nart_ctx* ctx, int variant) {
     if (!ctx) return NART_E_INVALID;
     for (nart_ctx* c : ctx->subs)
         if (int rc = nart_hip_set_variant(c, variant)) return fail(ctx, rc, c->err);
-    if (variant < 0 || variant > 3 || variant == 1)
-        return fail(ctx, NART_E_UNSUPPORTED, "variant must be 0 (megakernel with a wave ray queue), 2 (megakernel, "
-                                             "traversal quorum always) or 3 (megakernel, quorum by rounds); the "
-                                             "wavefront variant 1 was retired (2x slower, DESIGN.md)");
+    if (variant != 0 && variant != 3)
+        return fail(ctx, NART_E_UNSUPPORTED, "variant must be 0 (megakernel with a wave ray queue) or 3 (megakernel, "
+                                             "one lane per pixel); the wavefront variant 1 and the traversal-quorum "
+                                             "variant 2 were retired (DESIGN.md)");
     ctx->variant = variant;
     return NART_OK;
 }
@@ -1955,7 +1965,7 @@ int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t
         r2.lds_nodes = render_lds_nodes(ctx, rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK), NART_RQ_BLOCK / 256);
         const size_t lds_rq = rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK) + (size_t)r2.lds_nodes * sizeof(BVHNode);
         static bool attr = false;
-        auto kern = k_render_rq<10, false, false>;
+        auto kern = k_render_rq<false, false, false>;
         if (!attr) {
             hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             attr = true;

@@ -254,6 +254,36 @@ def materials(directory=None, width=320, height=240, spp=16):
     return path
 
 
+def nested_glass(directory=None, width=48, height=36, spp=4, n=14, bounces=32):
+    """n concentric smooth glass spheres (radius 0.1 k, priority rising inward, eta alternating
+    1.5 / 1.2) in front of a lambert backdrop, lit by a disk light: a camera ray through the
+    middle crosses n interfaces inward, so the nested-dielectric list (pathintegrator.h:9-19)
+    grows to n entries -- beyond the 10 the path kernels keep in registers."""
+    d = directory or tempfile.mkdtemp(prefix="nart_nested_")
+    os.makedirs(d, exist_ok=True)
+    jm = []
+    for k in range(n):
+        name = "shell%02d" % k
+        write_geo(os.path.join(d, name + ".geo"), *_uv_sphere((0.0, 0.0, 1.0), 0.1 * (n - k), 10, 20))
+        jm.append({"filePath": os.path.join(d, name + ".geo"), "priority": k + 1,
+                   "material": {"type": "glass", "rho_s": [1, 1, 1], "tau": [1, 1, 1],
+                                "eta": 1.5 if k % 2 == 0 else 1.2, "roughness": 0}})
+    write_geo(os.path.join(d, "back.geo"), *_uv_grid((-4, 3, -2), (8, 0, 0), (0, 0, 6), (0, -1, 0), 4))
+    jm.append({"filePath": os.path.join(d, "back.geo"), "material": {"type": "lambert", "rho_d": [0.6, 0.5, 0.4]}})
+    scene = {
+        "renderSessions": [{"imageWidth": width, "imageHeight": height, "bucketSize": 8, "spp": spp,
+                            "bounces": bounces, "filterWidth": 1.5, "rougheningFactor": 0.0}],
+        "camera": {"fov": 20.0, "transform": [1, 0, 0, 0, 0, 0, -1, -7.0, 0, 1, 0, 1.0, 0, 0, 0, 1]},
+        "meshes": jm,
+        "lights": [{"type": "disk", "radius": 0.8, "Le": [1.0, 0.95, 0.9], "intensity": 40.0,
+                    "transform": [1, 0, 0, 0.0, 0, 0, 1, -3.0, 0, -1, 0, 3.0, 0, 0, 0, 1]}],
+    }
+    path = os.path.join(d, "nested.json")
+    with open(path, "w") as f:
+        json.dump(scene, f, indent=1)
+    return path
+
+
 def sky_texture(width=128, height=64, sun=(0.3, 0.35), sun_size=0.035, sun_power=60.0):
     """Equirect sky (row 0 = zenith): blue-to-white gradient, dark ground, Gaussian sun.  Fixed
     formula, no RNG."""

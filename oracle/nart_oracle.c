@@ -1165,6 +1165,14 @@ static v3 estimate_direct(const oracle_scene* s, worker_t* w, v3 wo, const bsdf_
     return muls3(L, numLights);
 }
 
+/* test statistic: the longest IntersectionInfo list any path reached (oracle_max_list) */
+static uint32_t g_max_list = 0;
+uint32_t oracle_max_list(int reset) {
+    const uint32_t v = __atomic_load_n(&g_max_list, __ATOMIC_RELAXED);
+    if (reset) __atomic_store_n(&g_max_list, 0u, __ATOMIC_RELAXED);
+    return v;
+}
+
 /* PathIntegrator::Li_alpha (pathintegrator.cpp:144-259) */
 static v4 li_alpha(const oracle_scene* s, worker_t* w, rng_t* rng, ray_t ray, const nart_render_params* p) {
     iinfo_t list[64];
@@ -1222,7 +1230,13 @@ static v4 li_alpha(const oracle_scene* s, worker_t* w, rng_t* rng, ray_t ray, co
                 float bsdfSample = rng_float(rng);
                 eta_sampled = bsdf_sample_eta(&bsdf, bsdfSample);
             }
-            if (flags & F_TRANSMISSIVE) update_isect_list(list, &nlist, &is, eta_sampled);
+            if (flags & F_TRANSMISSIVE) {
+                update_isect_list(list, &nlist, &is, eta_sampled);
+                uint32_t m = __atomic_load_n(&g_max_list, __ATOMIC_RELAXED);
+                while (nlist > m && !__atomic_compare_exchange_n(&g_max_list, &m, nlist, 1, __ATOMIC_RELAXED,
+                                                                 __ATOMIC_RELAXED)) {
+                }
+            }
             float q = gmax((beta.x + beta.y + beta.z) * 0.33333f, 0.f);
             if (bounce > 3) {
                 if (q >= rng_float(rng)) beta = divs3(beta, q);

@@ -54,6 +54,8 @@ void oracle_latin_square(uint32_t seed, uint32_t spp, float* out_xy, uint32_t* r
 float oracle_fresnel(float eta_o, float eta_i, float cos_theta);
 /* BinarySearch (util.cpp:4-20) as the environment light's CDF inversion uses it. */
 uint32_t oracle_binary_search(float value, const float* v, uint32_t start, uint32_t end);
+/* Test statistic: the longest nested-dielectric list a path of this process reached (reset: zero it). */
+uint32_t oracle_max_list(int reset);
 
 #ifdef __cplusplus
 }

@@ -78,6 +78,8 @@ def lib():
         _lib.oracle_fresnel.restype = ctypes.c_float
         _lib.oracle_binary_search.argtypes = [ctypes.c_float, P, ctypes.c_uint32, ctypes.c_uint32]
         _lib.oracle_binary_search.restype = ctypes.c_uint32
+        _lib.oracle_max_list.argtypes = [ctypes.c_int]
+        _lib.oracle_max_list.restype = ctypes.c_uint32
         _lib.oracle_camera_ray.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                            ctypes.c_float, ctypes.c_float, P, P]
         _lib.oracle_trace.argtypes = [P, P, P, ctypes.c_float, P]
@@ -170,3 +172,8 @@ def trace(orc, o, d, tmax=float("inf")):
     t0 = np.array([out[1]], np.int32).view(np.float32)[0]
     t1 = np.array([out[3]], np.int32).view(np.float32)[0]
     return out[0], float(t0), out[2], float(t1)
+
+
+def max_list_length(reset=False):
+    """Longest nested-dielectric list (pathintegrator.h:9-19) any oracle path reached."""
+    return int(lib().oracle_max_list(1 if reset else 0))
