@@ -113,7 +113,9 @@ def load_profile(tag):
     the committed summary, and only if it was measured on the current kernel sources
     (hip_source_sha); otherwise None and the source says why."""
     from nart_amd.build import hip_source_sha
-    path = os.path.join(REPO, "profiles", "pmc_latest.json")
+    path = os.path.join(REPO, "profiles", "pmc_latest_%s.json" % tag)
+    if not os.path.exists(path):
+        path = os.path.join(REPO, "profiles", "pmc_latest.json")
     if not os.path.exists(path):
         return None, "no committed PMC summary"
     try:

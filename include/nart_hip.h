@@ -57,6 +57,7 @@ typedef struct nart_render_stats {
 #define NART_SCHED_VOL_SPARSE  0x20u /* volume kernel: sparse waves for the costliest groups       */
 #define NART_SCHED_SPLAT_SKEW  0x40u /* skewed-time splat (k_splat_skew)                           */
 #define NART_SCHED_PRIMARY     0x80u /* camera rays traced first (k_primary)                       */
+#define NART_SCHED_SPLAT_ROWS  0x100u /* skewed-time splat, W lanes per tile column (k_splat_rows)  */
 
 /* Upload the scene, build the device BVH.  device_id: HIP ordinal. */
 int nart_hip_create(const nart_scene_blob* scene, int device_id, nart_ctx** out);
@@ -179,8 +180,9 @@ int nart_hip_context_bvh(const nart_ctx* ctx, nart_bvh_info* out, double* build_
 int nart_hip_set_variant(nart_ctx* ctx, int variant);
 
 /* Splat kernel (all bit-identical): -1 = automatic (the default: 4 when the launch fills >= 1
-   wave per SIMD, else 3), 4 = skewed-time tile columns over the pixel-major sample layout (each
-   sample fetched once per bucket), 3 = four tile pixels per lane over the sample-major layout;
+   wave per SIMD, else 5), 4 = skewed-time tile columns over the pixel-major sample layout (each
+   sample fetched once per bucket), 5 = the same with one lane per (tile column, row class), for
+   small launches, 3 = four tile pixels per lane over the sample-major layout;
    1, 0 = one tile pixel per lane with the threshold / direct filter-index arithmetic (2 = 1).
    Modes fall back to a lower one where their preconditions (power-of-two buckets <= 32, filter
    bounds 1-3, threshold table and weight LUT) do not hold.  (An LDS-staged mode, an unskewed

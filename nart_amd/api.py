@@ -60,7 +60,7 @@ class BvhInfo(ctypes.Structure):
 
 # nart_render_stats.schedule bits (include/nart_hip.h NART_SCHED_*)
 SCHED = {"probe_queue": 0x1, "priority": 0x2, "spec_pairs": 0x4, "wave_groups": 0x8, "vol_queue": 0x10,
-         "vol_sparse": 0x20, "splat_skew": 0x40, "primary": 0x80}
+         "vol_sparse": 0x20, "splat_skew": 0x40, "primary": 0x80, "splat_rows": 0x100}
 
 
 class RenderStats(ctypes.Structure):
@@ -176,7 +176,9 @@ def hip_lib():
             scene_lib()  # its directory is on the alternative build's rpath too
             lib = ctypes.CDLL(os.path.abspath(alt))
             for fn, (res, args) in _HIP_SIGS.items():
-                f = getattr(lib, fn)
+                f = getattr(lib, fn, None)  # an older build may lack newer entry points
+                if f is None:
+                    continue
                 f.restype = res
                 f.argtypes = args
             _libs["libnart_hip.so"] = lib
@@ -358,8 +360,9 @@ class HipRenderer:
 
     def set_splat_mode(self, mode):
         """-1 = automatic (default: the skewed-time splat on launches of >= 1 wave per SIMD, else
-        four tile pixels per lane), 4 = skewed-time splat, 3 = four tile pixels per lane, 2-0 = one
-        pixel per lane (include/nart_hip.h); identical results."""
+        its W-lanes-per-column form), 5 = skewed time with W lanes per tile column, 4 = skewed-time
+        splat, 3 = four tile pixels per lane, 1-0 = one pixel per lane (include/nart_hip.h);
+        identical results."""
         self._check(self._lib.nart_hip_set_splat_mode(self._ctx, int(mode)))
 
     def _check(self, rc):

@@ -143,9 +143,8 @@ struct RenderArgs {
     // k_render_rq: queue entries with bit 31 set are priority pixels (the costliest of a small
     // shard): their rays are traced first and the traversal phase ends as soon as they resolve
     uint32_t rq_prio = 0;
-    // k_render_rq with rq_prio: also end a traversal phase once this many priority lanes have all
-    // their results while other priority rays are still in flight (0: only when all are resolved)
-    uint32_t rq_early = 0;
+    // k_render_rq: issue priority (s_setprio) of waves while they hold priority pixels (0: none)
+    uint32_t rq_setprio = 0;
     // k_render_rq: entries with bit 30 set too are pixels dealt to two adjacent lanes, which run
     // the pixel's sample chain with RNG speculation (see k_render_rq); the queue then holds
     // qlen entries (the first round's pixels twice), not n_slots
@@ -166,6 +165,7 @@ struct RenderArgs {
 };
 #define RQ_PRIO_BIT 0x80000000u
 #define RQ_PAIR_BIT 0x40000000u
+#define RQ_QUAD_BIT 0x20000000u  // with RQ_PAIR_BIT: the pixel's group has four lanes, not rq_pairs
 
 // xorshift32 state after n draws (rng.h:38-40 applied n times)
 ND uint32_t rng_jump(uint32_t y, uint32_t n) {
@@ -1123,6 +1123,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
     // while its rays are still in flight).  pF / pR: the chain frontier (first sample not yet
     // written) and its true start state; bm: majority vote over the draw counts (val | cnt << 16).
     bool pm = false;
+    uint32_t pQ = 1;  // lanes of this pixel's speculative group (rq_pairs, or 4 with RQ_QUAD_BIT)
     uint32_t jfl = 0, jst = 0, jend = 0, nd = 0, pF = 0, pR = 0, bm = 0;
     float4 jres = make_float4(0.f, 0.f, 0.f, 0.f);
     enum { J_VER = 1, J_FIN = 2, J_DOOM = 4 };
@@ -1133,7 +1134,8 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
         c_s = 0xFFFFFFFFu;
         prio = A.rq_prio && (sl & RQ_PRIO_BIT);
         pm = A.rq_pairs && (sl & RQ_PAIR_BIT);
-        if (A.rq_prio) sl &= ~(RQ_PRIO_BIT | RQ_PAIR_BIT);
+        pQ = (A.rq_pairs && (sl & RQ_QUAD_BIT)) ? 4u : (A.rq_pairs ? A.rq_pairs : 1u);
+        if (A.rq_prio) sl &= ~(RQ_PRIO_BIT | RQ_PAIR_BIT | RQ_QUAD_BIT);
         slot = sl;
         const uint32_t xy = A.slot_xy[sl];
         px = xy & 0xFFFFu;
@@ -1152,7 +1154,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
         bm = 0;
         jst = rng;
         jfl = J_VER;
-        if (lane & (A.rq_pairs - 1u)) {
+        if (lane & (pQ - 1u)) {
             s = A.spp;
             jfl = 0;
         }
@@ -1257,10 +1259,19 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
         if (COUNT) ++n_ext;
     };
 
+    bool raised = false;  // this wave runs at a raised issue priority (A.rq_setprio)
     for (;;) {
         // ---------------- path phase
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         newk = 0;
+        if (A.rq_setprio) {
+            const bool want = __ballot(prio && (pm || waiting || s < A.spp)) != 0;
+            if (want != raised) {
+                if (want) __builtin_amdgcn_s_setprio(2);
+                else __builtin_amdgcn_s_setprio(0);
+                raised = want;
+            }
+        }
 #ifdef NART_WAVEPROF
         if (COUNT && lane == 0) cnt.pw[10]++;  // path phases
         const uint64_t prof_tp = __builtin_amdgcn_s_memtime();
@@ -1307,7 +1318,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
         // contiguous run of samples [pF, hs]; a job becomes verified when it reaches the frontier
         // with the frontier's true start state, otherwise every job of the run is dropped.
         if (A.rq_pairs) {
-            const uint32_t Q = A.rq_pairs, gb = (uint32_t)lane & ~(Q - 1u), mi = (uint32_t)lane & (Q - 1u);
+            const uint32_t Q = pQ, gb = (uint32_t)lane & ~(Q - 1u), mi = (uint32_t)lane & (Q - 1u);
             const uint32_t NONE = A.spp;
             uint32_t gs[4], gst[4], gfl[4], gend[4], gnd[4];
             bool gw[4], gchg[4];
@@ -1772,16 +1783,14 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
                 cp_last = now;
             }
 #endif
-            // priority rays all resolved and a priority lane waits on its results: shade it now
+            // priority rays all resolved and a priority lane waits on its results: shade it now (ending
+            // the phase as soon as 1/2/4/8 priority lanes were ready, with other priority rays still in
+            // flight, measured slower: C3 1/8 shard 121/114/102/94 vs 90 ms, profiles/r05d_rq_early_ab.log
+            // -- more path phases, each costing the union of the wave's shading branches; and letting
+            // the other lanes sit out the path phases the priority rule starts unless 8 / 24 / 64 of
+            // them are ready: 89.9 / 91.0 / 94.4 vs 88.9 ms)
             if (A.rq_prio && ph == pt && __ballot(tracing && tr_prio) == 0 && __ballot(waiting && prio) != 0) break;
-            if (A.rq_early) {
-                bool ready = false;
-                if (waiting && prio) {
-                    const uint4 r = *my_res;
-                    ready = (!ext_pending || r.x != RQ_PENDING) && (!use1 || r.y != 2u) && (!use2 || r.z != 2u);
-                }
-                if ((uint32_t)__popcll(__ballot(ready)) >= A.rq_early) break;
-            }
+
             if (ph == pt && nh == nt && (uint32_t)__popcll(__ballot(tracing)) <= A.rq_quorum) break;
         }
 #ifdef NART_WAVEPROF
@@ -2456,6 +2465,213 @@ __global__ __launch_bounds__(256) void k_splat_skew(SplatArgs A) {
     // y wrap: last-row samples into tile rows 0 .. 2R+1 (the first band's), after all their other
     // sources, in the raster order of their source columns, the extra column last
     if (tr0 == 0 && bh == B) {
+        for (int sx = max(0, (int)tx - 2 * R); sx <= min(bw - 1, (int)tx); ++sx)
+            if ((flagY >> sx) & 1u) ywrap_pass(sx);
+        if (xwrap_lane && ((flagY >> (bw - 1)) & 1u)) ywrap_pass(bw - 1);
+    }
+}
+
+// The skewed-time splat with the W = 2R+1 window rows of a tile column on W lanes instead of one
+// (k_splat_rows, launches too small to fill the GPU with k_splat_skew's one lane per column).
+// Lane (k, tx) of a bucket owns the tile rows r = k (mod W) of column tx, one at a time: at step t
+// it takes the same source (sy, sx) as k_splat_skew's lane tx and adds each sample to the one row
+// r in [sy, sy + 2R] with r = k (mod W), r = sy + ((k - sy) mod W), with k_splat_skew's operations
+// for that row (ys = yb + (r - sy), the same hit test, d2, LUT cell and packed products).  A row's
+// sources still arrive in raster order (t = W sy + sx), and a class's rows in increasing order, so
+// a lane writes row r once the next source needs row r + W (rows without sources are written as
+// zeros).  Five times the lanes of k_splat_skew, each doing the work of one row per sample
+// (one accumulator, few registers); the W lanes of a column load the same sample (one L1 line).
+// Bucket-edge wraps as in k_splat_skew: the extra column source (sy, B-1) after the lane's last
+// source of row sy; y wraps into the written rows 0..2R+1 read back after all regular steps.
+#ifndef NART_ROWS_PF
+#define NART_ROWS_PF 4  // samples per group; the next group is in flight (few waves: latency-bound)
+#endif
+template <int R>
+__global__ __launch_bounds__(512) void k_splat_rows(SplatArgs A) {
+    constexpr int W = 2 * R + 1, NWR = 2 * R + 2;
+    extern __shared__ __attribute__((aligned(16))) float4 s_dyn4[];
+    float4* s_lut = s_dyn4;
+    const uint32_t T = A.tile, U = T * (uint32_t)W, UB = blockDim.x / U;  // lanes per bucket, buckets per block
+    uint32_t* s_flag = reinterpret_cast<uint32_t*>(s_dyn4 + A.lut_n);    // [bucket of block][x, y]
+    for (uint32_t i = threadIdx.x; i < A.lut_n; i += blockDim.x) s_lut[i] = A.lut[i];
+    if (threadIdx.x < 2u * UB) s_flag[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint32_t lb = threadIdx.x / U, j = threadIdx.x % U;
+    const uint32_t k = j / T, tx = j % T;
+    const uint32_t bi = blockIdx.x * UB + lb;
+    const bool live = lb < UB && bi < A.n_buckets;
+    uint32_t* flag = s_flag + 2u * (lb < UB ? lb : 0u);
+    uint32_t bid = 0, x0 = 0, y0 = 0, base = 0;
+    int bw = 0, bh = 0;
+    const int B = (int)A.B;
+    if (live) {
+        bid = A.bucket_ids[bi];
+        x0 = A.B * (bid % A.nbx);
+        y0 = A.B * (bid / A.nbx);
+        bw = (int)(min(x0 + A.B, A.totalW) - x0);
+        bh = (int)(min(y0 + A.B, A.totalH) - y0);
+        base = A.bucket_base[bi];
+    }
+    const float fw = A.fw;
+    const float edgeX = (float)(x0 + A.B + A.fb), edgeY = (float)(y0 + A.B + A.fb);
+    // pre-pass: which last-column sources (bit sy) / last-row sources (bit sx) have wrapping samples
+    if (live) {
+        for (int q = (int)j; q < 2 * B; q += (int)U) {
+            const bool colsrc = q < B;
+            const int sy = colsrc ? q : B - 1, sx = colsrc ? B - 1 : q - B;
+            if ((colsrc && bw != B) || (!colsrc && bh != B) || sy >= bh || sx >= bw) continue;
+            const float2* sp = A.samples + (size_t)(base + (uint32_t)(sy * bw + sx)) * A.spp;
+            const float f = colsrc ? (float)(x0 + (uint32_t)sx + A.fb) : (float)(y0 + (uint32_t)sy + A.fb);
+            const float edge = colsrc ? edgeX : edgeY;
+            bool any = false;
+            for (uint32_t i = 0; i < A.spp && !any; ++i) {
+                const float2 u = sp[i];
+                any = (f + (colsrc ? u.x : u.y)) >= edge;
+            }
+            if (any) atomicOr(flag + (colsrc ? 0 : 1), 1u << (colsrc ? sy : sx));
+        }
+    }
+    __syncthreads();
+    if (!live) return;
+    const uint32_t flagX = flag[0], flagY = flag[1];
+    const float xsA = (float)(tx + x0), xsB = (float)(tx + x0 + A.B);
+    const int lut_b0 = (int)A.lut_b0, lut_last = (int)A.lut_n - 1;
+    const uint32_t tpx = T * T;
+    float* out = A.tiles + ((uint64_t)bi * tpx + tx) * 5;  // + row * T * 5
+    nd_f2v cxy = nd_f2v{0.f, 0.f}, czw = nd_f2v{0.f, 0.f};
+    float cws = 0.f;
+    int wr = (int)k;  // the open row of this lane's class
+    auto write_row = [&]() {
+        float* o = out + (size_t)wr * T * 5;
+        o[0] = cxy.x;
+        o[1] = cxy.y;
+        o[2] = czw.x;
+        o[3] = czw.y;
+        o[4] = cws;
+        cxy = nd_f2v{0.f, 0.f};
+        czw = nd_f2v{0.f, 0.f};
+        cws = 0.f;
+        wr += W;
+    };
+    // one sample into row r (the lane's open row): k_splat_skew's operations for that row.  (Issuing
+    // a sample group's LUT reads together with select accumulation measured no faster here: C3 1/2,
+    // 1/4 shards 15.4 / 8.6 vs 14.6 / 7.9 ms, profiles/r05e_splat_rows_ab.log)
+    float fx = 0.f, ybA = 0.f, ybB = 0.f, fy = 0.f, dk = 0.f;  // dk = r - sy
+    auto splat_r = [&](float2 uv, float4 L) {
+        const float scx = fx + uv.x, scy = fy + uv.y;
+        const float xs = scx >= edgeX ? xsB : xsA;
+        const bool xhit = (scx - fw) < xs + 1.f && xs < (scx + fw);
+        const float distX = (xs + 0.5f) - scx;
+        const float dx2 = distX * distX;
+        const float yb = scy >= edgeY ? ybB : ybA;
+        const float ys = yb + dk;
+        const float dy = (ys + 0.5f) - scy;
+        const float d2 = dx2 + dy * dy;
+        const float4 e = s_lut[lut_cell(d2, lut_b0, lut_last)];
+        const float w = d2 >= e.x ? e.z : e.y;
+        if (xhit && (scy - fw) < ys + 1.f && ys < (scy + fw)) {
+            const nd_f2v w2 = nd_f2v{w, w};
+            cxy += nd_f2v{L.x, L.y} * w2;
+            czw += nd_f2v{L.z, L.w} * w2;
+            cws += w;
+        }
+    };
+    auto source_pass = [&](int sy, int sx) {  // every sample of bucket-local pixel (sx, sy)
+        const size_t first = (size_t)(base + (uint32_t)(sy * bw + sx)) * A.spp;
+        const float2* sp = A.samples + first;
+        const float4* lp = A.Lout + first;
+        fx = (float)(x0 + (uint32_t)sx + A.fb);
+        constexpr uint32_t PF = NART_ROWS_PF;
+        uint32_t i = 0;
+        float2 nu[PF];
+        float4 nL[PF];
+        if (A.spp >= PF) {
+#pragma unroll
+            for (uint32_t u = 0; u < PF; ++u) {
+                nu[u] = sp[u];
+                nL[u] = lp[u];
+            }
+        }
+        for (; i + PF <= A.spp; i += PF) {
+            float2 uv[PF];
+            float4 Lv[PF];
+#pragma unroll
+            for (uint32_t u = 0; u < PF; ++u) {
+                uv[u] = nu[u];
+                Lv[u] = nL[u];
+            }
+            if (i + 2 * PF <= A.spp) {
+#pragma unroll
+                for (uint32_t u = 0; u < PF; ++u) {
+                    nu[u] = sp[i + PF + u];
+                    nL[u] = lp[i + PF + u];
+                }
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < PF; ++u) splat_r(uv[u], Lv[u]);
+        }
+        for (; i < A.spp; ++i) splat_r(sp[i], lp[i]);
+    };
+    const bool xwrap_lane = bw == B && (int)tx <= 2 * R + 1 && bw - 1 > (int)tx;
+    const int tmax = W * (B - 1) + (B - 1);  // wave-uniform step count (k_splat_skew's, one band)
+    for (int t = 0; t <= tmax; ++t) {
+        const int d = (((int)tx - t) % W + W) % W;
+        const int sx = (int)tx - d, sy = (t - sx) / W;
+        if (sx < 0 || sx >= bw || sy < 0 || sy >= bh) continue;
+        const int r = sy + (((int)k - sy) % W + W) % W;  // this class's row in [sy, sy + 2R]
+        while (wr < r) write_row();
+        fy = (float)(y0 + (uint32_t)sy + A.fb);
+        ybA = (float)(y0 + (uint32_t)sy);
+        ybB = (float)(y0 + A.B + (uint32_t)sy);
+        dk = (float)(r - sy);
+        source_pass(sy, sx);
+        if (xwrap_lane && sx == (int)tx && ((flagX >> sy) & 1u)) source_pass(sy, bw - 1);  // the extra column
+    }
+    while (wr < (int)T) write_row();
+    // y wrap: last-row samples into tile rows 0 .. 2R+1 of this class, after all their other
+    // sources, in the raster order of their source columns, the extra column last
+    if (bh == B) {
+        const int nr = min(NWR, B - 1);
+        const float ysB0 = (float)(y0 + A.B);
+        auto ywrap_pass = [&](int sx) {
+            const int sy = B - 1;
+            const size_t first = (size_t)(base + (uint32_t)(sy * bw + sx)) * A.spp;
+            const float2* sp = A.samples + first;
+            const float4* lp = A.Lout + first;
+            const float fxw = (float)(x0 + (uint32_t)sx + A.fb), fyw = (float)(y0 + (uint32_t)sy + A.fb);
+            for (int rr = (int)k; rr < nr; rr += W) {
+                float acc[5];
+#pragma unroll
+                for (int c = 0; c < 5; ++c) acc[c] = out[(size_t)rr * T * 5 + c];
+                const float ys = ysB0 + (float)rr;
+                for (uint32_t i = 0; i < A.spp; ++i) {
+                    const float2 uv = sp[i];
+                    const float scx = fxw + uv.x, scy = fyw + uv.y;
+                    if (!(scy >= edgeY)) continue;
+                    const float4 L = lp[i];
+                    const float xs = scx >= edgeX ? xsB : xsA;
+                    const bool xhit = (scx - fw) < xs + 1.f && xs < (scx + fw);
+                    const float distX = (xs + 0.5f) - scx;
+                    const float dx2 = distX * distX;
+                    const bool hit = xhit && (scy - fw) < ys + 1.f && ys < (scy + fw);
+                    const float distY = (ys + 0.5f) - scy;
+                    const float d2 = dx2 + distY * distY;
+                    int cell = (int)(__float_as_uint(d2) >> 16) - lut_b0;
+                    cell = cell < 0 ? 0 : (cell > lut_last ? lut_last : cell);
+                    const float4 e = s_lut[cell];
+                    const float w = d2 >= e.x ? e.z : e.y;
+                    if (hit) {
+                        acc[0] += L.x * w;
+                        acc[1] += L.y * w;
+                        acc[2] += L.z * w;
+                        acc[3] += L.w * w;
+                        acc[4] += w;
+                    }
+                }
+#pragma unroll
+                for (int c = 0; c < 5; ++c) out[(size_t)rr * T * 5 + c] = acc[c];
+            }
+        };
         for (int sx = max(0, (int)tx - 2 * R); sx <= min(bw - 1, (int)tx); ++sx)
             if ((flagY >> sx) & 1u) ywrap_pass(sx);
         if (xwrap_lane && ((flagY >> (bw - 1)) & 1u)) ywrap_pass(bw - 1);

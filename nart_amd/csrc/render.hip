@@ -528,12 +528,29 @@ __global__ void k_flag_top(const uint32_t* sorted, uint32_t n, uint32_t E, uint3
 // costly pixel goes to Q adjacent lanes (Qj .. Qj + Q - 1) with RQ_PAIR_BIT too, and the queue is
 // n + (Q - 1)*k*W long.
 __global__ void k_build_queue(const uint32_t* top, const uint32_t* rest, uint32_t n, uint32_t W, uint32_t k,
-                              uint32_t prio, uint32_t pairs, uint32_t* queue) {
+                              uint32_t prio, uint32_t pairs, uint32_t half, uint32_t quad, uint32_t* queue) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t per = pairs ? pairs : 1u, kk = per * k;  // first-round lanes of the costly pixels
-    if (p >= n + (per - 1u) * k * W) return;
+    if (p >= n + (per - 1u) * k * W + (quad ? 2u * W : 0u)) return;
     const uint32_t g = 64u * W;
-    if (p < g) {
+    if (p < g && quad) {
+        // quad: each first-round wave's costliest pixel (ranks 0..W-1) on four lanes, its other k-1
+        // costly pixels on pairs
+        const uint32_t w = p / 64u, j = p % 64u, kq = kk + 2u;
+        if (j < 4u) queue[p] = top[w] | prio | RQ_PAIR_BIT | RQ_QUAD_BIT;
+        else if (j < kq) queue[p] = top[((j - 4u) / per + 1u) * W + w] | prio | RQ_PAIR_BIT;
+        else queue[p] = rest[w * (64u - kq) + (j - kq)];
+    } else if (p >= g && quad) {
+        queue[p] = rest[(64u - kk - 2u) * W + (p - g)];
+    } else if (p < g && half) {
+        // half: only the first 4 waves of each 8-wave block hold costly pixels (2k each), so each
+        // SIMD has one priority wave and one other wave
+        const uint32_t w = p / 64u, j = p % 64u, b = w / 8u, i = w % 8u, k2 = 2u * kk;
+        const uint32_t pw = b * 4u + i;  // priority wave index
+        const uint32_t roff = b * 8u * (64u - kk) + (i < 4u ? i * (64u - k2) : 4u * (64u - k2) + (i - 4u) * 64u);
+        if (i < 4u && j < k2) queue[p] = top[(j / per) * (W / 2u) + pw] | prio | (pairs ? RQ_PAIR_BIT : 0u);
+        else queue[p] = rest[roff + (i < 4u ? j - k2 : j)];
+    } else if (p < g) {
         const uint32_t w = p / 64u, j = p % 64u;
         queue[p] = j < kk ? (top[(j / per) * W + w] | prio | (pairs ? RQ_PAIR_BIT : 0u))
                           : rest[w * (64u - kk) + (j - kk)];
@@ -802,13 +819,19 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
                 const uint32_t Q = pe <= 0 ? 0u : (pe >= 4 ? 4u : 2u);
                 const uint32_t pbit = (rq && prio_on) ? RQ_PRIO_BIT : 0u;
                 const uint32_t pairs = (pbit && Q && Q * k <= 64u) ? Q : 0u;
-                const uint32_t qlen = n + (pairs ? (pairs - 1u) * k * W : 0u);
+                // NART_RQ_QUAD (A/B): each first-round wave's costliest pixel gets four lanes
+                const bool quad = pbit && pairs == 2u && 2u * k + 2u <= 64u && std::getenv("NART_RQ_QUAD") &&
+                                  std::atoi(std::getenv("NART_RQ_QUAD")) != 0;
+                const uint32_t qlen = n + (pairs ? (pairs - 1u) * k * W : 0u) + (quad ? 2u * W : 0u);
+                // NART_RQ_HALF (A/B): the costly pixels on half of the first-round waves (one per
+                // SIMD, 2k each) and those waves at a raised issue priority while they hold them
+                const bool half = pbit && rq && (W % 8u) == 0u && 2u * (pairs ? pairs : 1u) * k <= 64u &&
+                                  std::getenv("NART_RQ_HALF") && std::atoi(std::getenv("NART_RQ_HALF")) != 0;
                 hipLaunchKernelGGL(k_build_queue, dim3((qlen + 255) / 256), block, 0, st, ctx->d_vals[1], ctx->d_vals[0],
-                                   n, W, k, pbit, pairs, ctx->d_queue);
+                                   n, W, k, pbit, pairs, half ? 1u : 0u, quad ? 1u : 0u, ctx->d_queue);
+                b.rq_setprio = pbit && std::getenv("NART_RQ_SETPRIO") ? (uint32_t)std::atoi(std::getenv("NART_RQ_SETPRIO")) : 0u;
                 b.rq_prio = pbit ? 1u : 0u;
                 b.rq_pairs = pairs;
-                // NART_RQ_EARLY (A/B): end a traversal phase once that many priority lanes are ready
-                b.rq_early = pbit && std::getenv("NART_RQ_EARLY") ? (uint32_t)std::max(0, std::atoi(std::getenv("NART_RQ_EARLY"))) : 0u;
                 b.qlen = qlen;
                 if (pbit) ctx->sched |= NART_SCHED_PRIORITY;
                 if (pairs) ctx->sched |= NART_SCHED_SPEC_PAIRS;
@@ -1142,13 +1165,20 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
     // gain at the C3 1/2 shard (17 -> 12.5 ms) is within the path kernels' run-to-run spread under
     // the pixel-major layout (186-208 ms on one box; profiles/r03l_c3_half_shard_splat_ab.log).
     const double skew_from = p->integrator == NART_INTEGRATOR_VOLUME ? 0.5 * skew_min : skew_min;
-    const int splat_mode = ctx->splat_mode >= 0 ? ctx->splat_mode : (skew_waves >= skew_from * 4.0 * n_cus ? 4 : 3);
+    // Below that, k_splat_rows (mode 5: W lanes per tile column, five times k_splat_skew's
+    // parallelism, each sample still fetched once per bucket) unless NART_SPLAT_SMALL=col4
+    const char* ss = std::getenv("NART_SPLAT_SMALL");
+    const int small_mode = ss && std::strcmp(ss, "col4") == 0 ? 3 : 5;
+    const int splat_mode =
+        ctx->splat_mode >= 0 ? ctx->splat_mode : (skew_waves >= skew_from * 4.0 * n_cus ? 4 : small_mode);
     // NART_SKEW_BANDS (read per call): 1 or 2 forces the band count
     const char* be = std::getenv("NART_SKEW_BANDS");
     const uint32_t skew_bands = be && std::atoi(be) > 0 ? (std::atoi(be) >= 2 ? 2u : 1u)
                                                           : (skew_waves >= skew_min * 4.0 * n_cus ? 1u : 2u);
+    // skew: a pixel-major sample layout for k_splat_skew (mode 4) or k_splat_rows (mode 5)
     const bool skew = splat_mode >= 4 && lut_ok && (B & (B - 1)) == 0 && B <= 32 && tile <= 64 &&
                       g.filter_bounds >= 1 && g.filter_bounds <= 3;
+    const bool rows = skew && splat_mode == 5;
     if (lut_ok) {
         if (!ctx->d_lut) HIPCHK(hipMalloc(&ctx->d_lut, SPLAT_LUT_MAX * sizeof(float4)));
         HIPCHK(hipMemcpy(ctx->d_lut, lut.data(), lut.size() * sizeof(float4), hipMemcpyHostToDevice));
@@ -1266,7 +1296,15 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         // splat modes (all bit-identical): 4 skewed time, 3 four tile pixels per lane (power-of-two
         // buckets); 1 / 0 one tile pixel per lane with the threshold / direct filter-index arithmetic
         // (any bucket size; 2 selects 1 since the compare-only one-pixel kernel was retired)
-        if (skew) {
+        if (rows) {
+            ctx->sched |= NART_SCHED_SPLAT_ROWS;
+            const uint32_t U = g.tile_size * (2 * g.filter_bounds + 1), ub = std::max(1u, 512u / U);
+            const uint32_t threads = (ub * U + 63) / 64 * 64, nblk = (nbk + ub - 1) / ub;
+            const size_t lds = lut.size() * sizeof(float4) + 2u * ub * sizeof(uint32_t);
+            if (g.filter_bounds == 1) hipLaunchKernelGGL((k_splat_rows<1>), dim3(nblk), dim3(threads), lds, st, sa);
+            else if (g.filter_bounds == 2) hipLaunchKernelGGL((k_splat_rows<2>), dim3(nblk), dim3(threads), lds, st, sa);
+            else hipLaunchKernelGGL((k_splat_rows<3>), dim3(nblk), dim3(threads), lds, st, sa);
+        } else if (skew) {
             ctx->sched |= NART_SCHED_SPLAT_SKEW;
             const uint32_t nb = skew_bands;  // tile-row bands per bucket (k_splat_skew's NB)
             const uint32_t pb = 64u / g.tile_size, nblk = (nbk * nb + 4 * pb - 1) / (4 * pb);
@@ -1533,7 +1571,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
         const int var = std::atoi(v);
         if (var == 0 || var == 3) ctx->variant = var;
     }
-    if (const char* v = std::getenv("NART_SPLAT_MODE")) ctx->splat_mode = std::max(-1, std::min(4, std::atoi(v)));
+    if (const char* v = std::getenv("NART_SPLAT_MODE")) ctx->splat_mode = std::max(-1, std::min(5, std::atoi(v)));
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device_id || device_id < 0) {
         delete ctx;
@@ -1773,10 +1811,10 @@ int nart_hip_set_splat_mode(nart_ctx* ctx, int mode) {
     if (!ctx) return NART_E_INVALID;
     for (nart_ctx* c : ctx->subs)
         if (int rc = nart_hip_set_splat_mode(c, mode)) return fail(ctx, rc, c->err);
-    if (mode < -1 || mode > 4)
-        return fail(ctx, NART_E_UNSUPPORTED, "splat mode must be -1 (automatic) or 0-4 (4 skewed-time tile columns, 3 four pixels per "
-                                             "lane, 2-0 one pixel per lane; the LDS-staged and tile-column-sweep modes "
-                                             "were retired, DESIGN.md)");
+    if (mode < -1 || mode > 5)
+        return fail(ctx, NART_E_UNSUPPORTED, "splat mode must be -1 (automatic) or 0-5 (5 skewed-time tile rows, 4 skewed-time "
+                                             "tile columns, 3 four pixels per lane, 1-0 one pixel per lane; the "
+                                             "LDS-staged and tile-column-sweep modes were retired, DESIGN.md)");
     ctx->splat_mode = mode;
     return NART_OK;
 }

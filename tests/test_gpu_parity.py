@@ -107,13 +107,21 @@ def test_queue_scheduler_frames(gpu, glass_scene, monkeypatch, w, h, spp, prio):
     assert _bits_equal(g, r), _report(g, r)
 
 
-@pytest.mark.parametrize("pairs", ["2", "4", "0"], ids=["speculative-pairs", "speculative-quads", "single-lanes"])
-def test_queue_speculative_pairs(gpu, glass_scene, monkeypatch, pairs):
+@pytest.mark.parametrize("pairs,extra", [("2", ""), ("4", ""), ("0", ""), ("2", "NART_RQ_QUAD"), ("2", "NART_RQ_HALF"),
+                                         ("2", "NART_RQ_SETPRIO")],
+                         ids=["speculative-pairs", "speculative-quads", "single-lanes", "quad-top", "half-waves",
+                              "setprio"])
+def test_queue_speculative_pairs(gpu, glass_scene, monkeypatch, pairs, extra):
     """A shard of ~1.2 rounds of resident waves at 24 spp: the costliest pixels run as speculative
     lane pairs (one lane on the chain's frontier sample, the other on the next sample from a
     predicted RNG state; kept only when the prediction was exact).  Long enough chains for both
-    kept and dropped speculation; the frame must equal the oracle's bit for bit."""
+    kept and dropped speculation; the frame must equal the oracle's bit for bit.  Variants: four
+    lanes for every costly pixel, four for each first-round wave's costliest pixel only
+    (NART_RQ_QUAD), the costly pixels on half of the waves (NART_RQ_HALF), raised issue priority
+    (NART_RQ_SETPRIO)."""
     monkeypatch.setenv("NART_RQ_PAIRS", pairs)
+    if extra:
+        monkeypatch.setenv(extra, "1")
     p = _params(glass_scene, 512, 300, 24)
     g = nart_amd.HipRenderer(glass_scene, variant=0).render(p)
     r = oracle.Oracle(glass_scene).render(p)
@@ -373,7 +381,7 @@ def test_latin_square_high_spp_frame(gpu, glass_scene, glass_oracle):
 
 
 @pytest.mark.parametrize("bucket,fw", [(12, 2.0), (16, 1.0), (8, 2.5), (10, 0.75), (16, 3.0), (4, 0.25)])
-@pytest.mark.parametrize("splat_mode", [4, 3, 1, 0], ids=["skew", "col4", "threshold", "direct"])
+@pytest.mark.parametrize("splat_mode", [5, 4, 3, 1, 0], ids=["rows", "skew", "col4", "threshold", "direct"])
 def test_splat_bucket_and_filter_sizes(gpu, glass_scene, glass_oracle, bucket, fw, splat_mode):
     """Splat arithmetic paths: power-of-two buckets use the compare-only pair test, other sizes
     the direct one; filter widths with threshold-derived indices (fw > ~0.28) and without (0.25);
@@ -384,18 +392,20 @@ def test_splat_bucket_and_filter_sizes(gpu, glass_scene, glass_oracle, bucket, f
     assert _bits_equal(g, o), _report(g, o)
 
 
-@pytest.mark.parametrize("bands", [1, 2])
+@pytest.mark.parametrize("mode,bands", [(4, 1), (4, 2), (5, 0)], ids=["skew1", "skew2", "rows"])
 @pytest.mark.parametrize("which", ["glass", "materials", "env", "volume"])
-def test_skew_splat_frames(gpu, glass_scene, materials_scene, env_scene, volume_scenes, which, bands, monkeypatch):
-    """The skewed-time splat (forced: by default it runs only on launches of >= 1 wave per SIMD)
-    over the pixel-major sample layout, with one and two tile-row bands per bucket, on frames of
-    the path and volume integrators with filter widths 2 and 1.5 and ragged edge buckets, against
-    the oracle's framebuffer."""
-    monkeypatch.setenv("NART_SKEW_BANDS", str(bands))
+def test_skew_splat_frames(gpu, glass_scene, materials_scene, env_scene, volume_scenes, which, mode, bands,
+                           monkeypatch):
+    """The skewed-time splats over the pixel-major sample layout (forced: k_splat_skew runs by
+    default only on launches of >= 1 wave per SIMD, k_splat_rows below that), k_splat_skew with
+    one and two tile-row bands per bucket, on frames of the path and volume integrators with filter
+    widths 2 and 1.5 and ragged edge buckets, against the oracle's framebuffer."""
+    if bands:
+        monkeypatch.setenv("NART_SKEW_BANDS", str(bands))
     sc = {"glass": glass_scene, "materials": materials_scene, "env": env_scene,
           "volume": volume_scenes["c5"]}[which]
     p = _params(sc, 72, 40, 16)
-    g = nart_amd.HipRenderer(sc, splat_mode=4).render(p)
+    g = nart_amd.HipRenderer(sc, splat_mode=mode).render(p)
     r = oracle.Oracle(sc).render(p)
     assert _bits_equal(g, r), _report(g, r)
 
@@ -429,7 +439,7 @@ def _edge_wrap_buckets(p, n_each=2):
     raise AssertionError("no edge-wrap buckets found: xs %s ys %s corner %s" % (xs, ys, corner))
 
 
-@pytest.mark.parametrize("splat_mode,bands", [(4, 1), (4, 2), (3, 0)], ids=["skew1", "skew2", "col4"])
+@pytest.mark.parametrize("splat_mode,bands", [(4, 1), (4, 2), (5, 0), (3, 0)], ids=["skew1", "skew2", "rows", "col4"])
 def test_splat_bucket_edge_wraps(gpu, glass_scene, glass_oracle, splat_mode, bands, monkeypatch):
     """Edge-wrapped samples (x, y and the corner source with both) at their raster position in
     the tile pixels' sums: the skewed-time splat's flagged extra passes and the gather kernels'

@@ -20,11 +20,14 @@ def main():
     ap.add_argument("-s", type=int, default=16)
     ap.add_argument("--counters", action="store_true")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--bounces", type=int, default=0, help="override the scene's bounce limit")
     a = ap.parse_args()
     path = scenes.glass_sphere() if a.scene == "glass" else scenes.cornell()
     scene = nart_amd.Scene(path)
     p = nart_amd.load_sessions(path)[0]
     p.image_width, p.image_height, p.spp = a.w, a.H, a.s
+    if a.bounces:
+        p.bounces = a.bounces
     r = nart_amd.HipRenderer(scene)
     for rep in range(a.reps):
         st = nart_amd.RenderStats()

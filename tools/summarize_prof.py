@@ -77,13 +77,16 @@ def main(src, tag, config="1920x1080x256"):
             e["wait_inst_any"] = top.get("SQ_WAIT_INST_ANY", 0.0) / wc
         out["kernels"][k] = e
 
-    def timed(name, base):  # k_render_rq<MAXL, COUNT, ENV> / k_primary<COUNT, ENV>: COUNT == false
+    def timed(name, base):
+        # k_render_rq<EXT, COUNT, ENV> / k_primary<COUNT, ENV> / k_render_volume_sm<COUNT, WV>:
+        # the COUNT == false build is the timed one
         if not name.startswith("nd::" + base + "<"):
             return False
         args = [a.strip() for a in name.split("<", 1)[1].split(">", 1)[0].split(",")]
-        return "false" == (args[1] if base != "k_primary" else args[0])
+        return "false" == (args[1] if base == "k_render_rq" else args[0])
 
     rq = [k for k in out["kernels"] if timed(k, "k_render_rq")]
+    rq = rq or [k for k in out["kernels"] if timed(k, "k_render_volume_sm")]
     pr = [k for k in out["kernels"] if timed(k, "k_primary")]
     if rq and "hbm_bytes" in out["kernels"][rq[0]]:
         r = out["kernels"][rq[0]]
@@ -95,6 +98,8 @@ def main(src, tag, config="1920x1080x256"):
         out["lane_utilization"] = r.get("lane_utilization")
         out["valu_busy"] = r.get("valu_busy")
     json.dump(out, open(os.path.join(prof, tag + "_pmc.json"), "w"), indent=1)
+    # bench.py reads pmc_latest_<config>.json (and pmc_latest.json for the headline C3 config)
+    json.dump(out, open(os.path.join(prof, "pmc_latest_%s.json" % config), "w"), indent=1)
     if config == "1920x1080x256":
         json.dump(out, open(os.path.join(prof, "pmc_latest.json"), "w"), indent=1)
     print(json.dumps({k: v for k, v in out.items() if k != "kernels"}, indent=1))
