@@ -58,6 +58,7 @@ typedef struct nart_render_stats {
 #define NART_SCHED_SPLAT_SKEW  0x40u /* skewed-time splat (k_splat_skew)                           */
 #define NART_SCHED_PRIMARY     0x80u /* camera rays traced first (k_primary)                       */
 #define NART_SCHED_SPLAT_ROWS  0x100u /* skewed-time splat, W lanes per tile column (k_splat_rows)  */
+#define NART_SCHED_HALF_WAVES  0x200u /* costliest pixels on one wave per SIMD, raised priority     */
 
 /* Upload the scene, build the device BVH.  device_id: HIP ordinal. */
 int nart_hip_create(const nart_scene_blob* scene, int device_id, nart_ctx** out);

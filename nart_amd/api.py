@@ -60,7 +60,8 @@ class BvhInfo(ctypes.Structure):
 
 # nart_render_stats.schedule bits (include/nart_hip.h NART_SCHED_*)
 SCHED = {"probe_queue": 0x1, "priority": 0x2, "spec_pairs": 0x4, "wave_groups": 0x8, "vol_queue": 0x10,
-         "vol_sparse": 0x20, "splat_skew": 0x40, "primary": 0x80, "splat_rows": 0x100}
+         "vol_sparse": 0x20, "splat_skew": 0x40, "primary": 0x80, "splat_rows": 0x100,
+         "half_waves": 0x200}
 
 
 class RenderStats(ctypes.Structure):

@@ -1243,13 +1243,31 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
         return rng_float(rng);
     };
     // a sample's result: written at once, or held by a pair lane until verified
+#ifndef NART_PAIR_WRITES
+#define NART_PAIR_WRITES 0
+#endif
+    // NART_PAIR_WRITES: pixel-major rows keep an even sample's Li_alpha until the odd one after it
+    // and store both as one 32-B access (a lane's consecutive 16-B stores hit a line that was
+    // evicted in between)
+    float4 c_L = make_float4(0.f, 0.f, 0.f, 0.f);
+    bool c_held = false;
     auto end_sample = [&](float4 v) {
         if (pm) {
             jres = v;
             jend = rng;
             jfl |= J_FIN;
         } else {
-            A.Lout[soff + (uint64_t)s * sstr] = v;
+            const uint64_t si = soff + (uint64_t)s * sstr;
+            if (NART_PAIR_WRITES && !ENV && !EXT && !COUNT && c_held) {
+                typedef float v8f __attribute__((ext_vector_type(8)));
+                *reinterpret_cast<v8f*>(A.Lout + (si - 1u)) = v8f{c_L.x, c_L.y, c_L.z, c_L.w, v.x, v.y, v.z, v.w};
+                c_held = false;
+            } else if (NART_PAIR_WRITES && !ENV && !EXT && !COUNT && sstr == 1u && (si & 1u) == 0u && s + 1u < A.spp) {
+                c_L = v;
+                c_held = true;
+            } else {
+                A.Lout[si] = v;
+            }
             ++s;
         }
     };

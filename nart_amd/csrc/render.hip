@@ -722,7 +722,11 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
             const dim3 eg((n + 255) / 256);
             // costly pixels per first-round wave: few when the shard is small (their serial chains
             // bound the frame), all 64 (packed, launched first) when there are many rounds
-            uint32_t k = R >= 3.0 ? 32u : 8u;  // measured on C3 shards of 1/2, 1/4, 1/8 of the frame
+            // the costly pixels on one wave per SIMD (NART_RQ_HALF=0: dealt over every wave; see below)
+            const bool half_want = rq && !(std::getenv("NART_RQ_HALF") && std::atoi(std::getenv("NART_RQ_HALF")) == 0);
+            // measured on C3 shards of 1/2, 1/4, 1/8 of the frame; with half_want 12 (2 x 12 on each
+            // priority wave): C3 1/8 shard mean of the 8 ranks 4/6/8/12/14/16: 95.2/88.8/81.4/80.9/81.3/81.6 ms
+            uint32_t k = R >= 3.0 ? 32u : (half_want ? 12u : 8u);
             // ray-queue kernel: wave-group refill from 6 rounds of resident waves (C3 1/2 shard, 8
             // rounds: 241 -> 235 ms; C4 batches, ~9 rounds: 1385 -> 1566 Msamples/s).  Below that a
             // wave of costly groups outlasts the rest (1/4 shard, 4 rounds: 146 -> 211 ms), and
@@ -823,13 +827,18 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
                 const bool quad = pbit && pairs == 2u && 2u * k + 2u <= 64u && std::getenv("NART_RQ_QUAD") &&
                                   std::atoi(std::getenv("NART_RQ_QUAD")) != 0;
                 const uint32_t qlen = n + (pairs ? (pairs - 1u) * k * W : 0u) + (quad ? 2u * W : 0u);
-                // NART_RQ_HALF (A/B): the costly pixels on half of the first-round waves (one per
-                // SIMD, 2k each) and those waves at a raised issue priority while they hold them
-                const bool half = pbit && rq && (W % 8u) == 0u && 2u * (pairs ? pairs : 1u) * k <= 64u &&
-                                  std::getenv("NART_RQ_HALF") && std::atoi(std::getenv("NART_RQ_HALF")) != 0;
+                // Half waves (default): the costly pixels on the first 4 waves of each 8-wave block,
+                // 2k each -- one such wave per SIMD -- and those waves at a raised issue priority
+                // (s_setprio 2, NART_RQ_SETPRIO) while they hold priority work, so the other wave
+                // of the SIMD fills their stalls instead of sharing issue with them.  C3 1/8 shard,
+                // every rank: mean 84.2 -> 80.9 ms, worst 87-92 -> 86.0 ms
+                // (profiles/r05h_chain_schedule_ab.log)
+                const bool half = pbit && half_want && (W % 8u) == 0u && 2u * (pairs ? pairs : 1u) * k <= 64u;
                 hipLaunchKernelGGL(k_build_queue, dim3((qlen + 255) / 256), block, 0, st, ctx->d_vals[1], ctx->d_vals[0],
                                    n, W, k, pbit, pairs, half ? 1u : 0u, quad ? 1u : 0u, ctx->d_queue);
-                b.rq_setprio = pbit && std::getenv("NART_RQ_SETPRIO") ? (uint32_t)std::atoi(std::getenv("NART_RQ_SETPRIO")) : 0u;
+                const char* spe = std::getenv("NART_RQ_SETPRIO");
+                b.rq_setprio = pbit ? (spe ? (uint32_t)std::max(0, std::atoi(spe)) : (half ? 1u : 0u)) : 0u;
+                if (half) ctx->sched |= NART_SCHED_HALF_WAVES;
                 b.rq_prio = pbit ? 1u : 0u;
                 b.rq_pairs = pairs;
                 b.qlen = qlen;

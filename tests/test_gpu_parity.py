@@ -107,21 +107,21 @@ def test_queue_scheduler_frames(gpu, glass_scene, monkeypatch, w, h, spp, prio):
     assert _bits_equal(g, r), _report(g, r)
 
 
-@pytest.mark.parametrize("pairs,extra", [("2", ""), ("4", ""), ("0", ""), ("2", "NART_RQ_QUAD"), ("2", "NART_RQ_HALF"),
-                                         ("2", "NART_RQ_SETPRIO")],
-                         ids=["speculative-pairs", "speculative-quads", "single-lanes", "quad-top", "half-waves",
-                              "setprio"])
+@pytest.mark.parametrize("pairs,extra", [("2", ""), ("4", ""), ("0", ""), ("2", "NART_RQ_QUAD=1"), ("2", "NART_RQ_HALF=0"),
+                                         ("2", "NART_RQ_SETPRIO=0")],
+                         ids=["speculative-pairs", "speculative-quads", "single-lanes", "quad-top", "all-waves",
+                              "no-setprio"])
 def test_queue_speculative_pairs(gpu, glass_scene, monkeypatch, pairs, extra):
     """A shard of ~1.2 rounds of resident waves at 24 spp: the costliest pixels run as speculative
     lane pairs (one lane on the chain's frontier sample, the other on the next sample from a
     predicted RNG state; kept only when the prediction was exact).  Long enough chains for both
-    kept and dropped speculation; the frame must equal the oracle's bit for bit.  Variants: four
-    lanes for every costly pixel, four for each first-round wave's costliest pixel only
-    (NART_RQ_QUAD), the costly pixels on half of the waves (NART_RQ_HALF), raised issue priority
-    (NART_RQ_SETPRIO)."""
+    kept and dropped speculation; the frame must equal the oracle's bit for bit.  The default puts
+    the costly pixels on one wave per SIMD at raised issue priority; variants: four lanes for every
+    costly pixel, four for each first-round wave's costliest pixel only (NART_RQ_QUAD), the costly
+    pixels dealt over every wave (NART_RQ_HALF=0), no raised priority (NART_RQ_SETPRIO=0)."""
     monkeypatch.setenv("NART_RQ_PAIRS", pairs)
     if extra:
-        monkeypatch.setenv(extra, "1")
+        monkeypatch.setenv(*extra.split("="))
     p = _params(glass_scene, 512, 300, 24)
     g = nart_amd.HipRenderer(glass_scene, variant=0).render(p)
     r = oracle.Oracle(glass_scene).render(p)
