@@ -391,6 +391,9 @@ __global__ __launch_bounds__(256) void k_latin_draws(RenderArgs A, LatinScratch 
 #ifndef NART_LATIN_PIPE
 #define NART_LATIN_PIPE 0  // 1: swap i+1's reads issued before swap i's writes (register fix-ups)
 #endif
+#ifndef NART_LATIN_HALF
+#define NART_LATIN_HALF 1  // the second half of the shuffle in three-stage batches (k_latin_perm)
+#endif
 __global__ __launch_bounds__(64) void k_latin_perm(RenderArgs A, LatinScratch L) {
     extern __shared__ __attribute__((aligned(16))) uint16_t s_idx[];
     const uint32_t lane = threadIdx.x, g = blockIdx.x;
@@ -446,10 +449,37 @@ __global__ __launch_bounds__(64) void k_latin_perm(RenderArgs A, LatinScratch L)
         // arrays carry PF padding rows), so that no branch sits between a load and its use: with
         // guarded loads the compiler waited for every outstanding load (vmcnt(0)) before each
         // swap, i.e. the prefetch did not hide the HBM latency.
+        //
+        // The second half of the shuffle needs no serial chain.  Step i swaps positions i and
+        // c_i <= n-1-i, so for i >= m = ceil(n/2): c_i < m, position i is touched by no other
+        // step from m on (step k touches k and c_k < m), and nothing after step i reads it.  A
+        // batch of steps i >= m is then exactly (1) B_i = A[i] for the whole batch, (2) in step
+        // order: r_i = A[c_i], A[c_i] = B_i, (3) A[i] = r_i: no LDS write waits for a read, where
+        // a swap waits for its two reads before writing them back (the first half keeps that).
+        const uint32_t m = (n + 1u) / 2u;
         uint32_t i2 = 0;
         for (; 2 * (i2 + PF) <= n; i2 += PF) {
 #pragma unroll
             for (uint32_t u = 0; u < PF; ++u) nxt[u] = c[(size_t)(i2 + PF + u) * 64];
+            if (NART_LATIN_HALF && 2 * i2 >= m) {  // wave-uniform
+                uint32_t bv[2 * PF], rv[2 * PF];
+#pragma unroll
+                for (uint32_t q = 0; q < 2 * PF; ++q) bv[q] = ix[(2 * i2 + q) * 64];
+#pragma unroll
+                for (uint32_t u = 0; u < PF; ++u) {
+#pragma unroll
+                    for (uint32_t h = 0; h < 2; ++h) {
+                        const uint32_t ci = (cur[u] >> (16 * h)) & 0xFFFFu;
+                        rv[2 * u + h] = ix[ci * 64];
+                        ix[ci * 64] = (uint16_t)bv[2 * u + h];
+                    }
+                }
+#pragma unroll
+                for (uint32_t q = 0; q < 2 * PF; ++q) ix[(2 * i2 + q) * 64] = (uint16_t)rv[q];
+#pragma unroll
+                for (uint32_t u = 0; u < PF; ++u) cur[u] = nxt[u];
+                continue;
+            }
 #pragma unroll
             for (uint32_t u = 0; u < PF; ++u) {
 #pragma unroll

@@ -62,3 +62,51 @@ def test_three_kernel_latin_square_matches_reference_order(built, n):
         got, state = _latin_three_kernels(seed, n)
         assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), (seed, n)
         assert state == want_state
+
+
+def _perm_batched(c, n, PF=16):
+    """k_latin_perm's replay (NART_LATIN_HALF): serial swaps in batches of 2 PF, except that a
+    full batch starting at or after m = ceil(n/2) runs as three stages (B_i = A[i]; in step order
+    r_i = A[c_i], A[c_i] = B_i; A[i] = r_i), the partial last batch serially."""
+    A = list(range(n + 2))
+    m, i2 = (n + 1) // 2, 0
+    while 2 * (i2 + PF) <= n:
+        idx = range(2 * i2, 2 * i2 + 2 * PF)
+        if 2 * i2 >= m:
+            bv = [A[i] for i in idx]
+            rv = []
+            for q, i in enumerate(idx):
+                rv.append(A[c[i]])
+                A[c[i]] = bv[q]
+            for q, i in enumerate(idx):
+                A[i] = rv[q]
+        else:
+            for i in idx:
+                A[i], A[c[i]] = A[c[i]], A[i]
+        i2 += PF
+    for i in range(2 * i2, n):
+        A[i], A[c[i]] = A[c[i]], A[i]
+    return A[:n]
+
+
+@pytest.mark.parametrize("n", [31, 32, 64, 65, 96, 100, 129, 256, 257, 511, 512, 1023, 1024])
+def test_second_half_three_stage_shuffle_matches_serial(n):
+    """For i >= ceil(n/2) the choices c_i <= n-1-i fall below the batch, so the three-stage form
+    of k_latin_perm's second half equals the serial swaps, on random and on RNG-drawn choices."""
+    r = np.random.default_rng(n)
+    for t in range(40):
+        if t % 2:
+            c = [int(r.integers(0, n - i)) for i in range(n)]
+        else:  # the pixel's own draws (sampling.cpp:81-84), x then y
+            rng = (t * 7919 + 2463534242) & M32
+            for _ in range(2 * n):
+                rng = _xorshift(rng)
+            c = []
+            for i in range(n):
+                rng = _xorshift(rng)
+                c.append((((rng * 0x9E3779B9) & M32) * (n - i)) >> 32)
+                rng = _xorshift(rng)
+        want = list(range(n))
+        for i in range(n):
+            want[i], want[c[i]] = want[c[i]], want[i]
+        assert _perm_batched(c, n) == want

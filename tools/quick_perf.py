@@ -21,8 +21,23 @@ def main():
     ap.add_argument("--counters", action="store_true")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--bounces", type=int, default=0, help="override the scene's bounce limit")
+    ap.add_argument("--env", type=int, default=1024, help="c4: environment map width (height = width / 2)")
+    ap.add_argument("--flat", default="", help="c4 diagnostics: comma list of rho_d,roughness,normal to replace "
+                                               "by constants (not a parity configuration)")
     a = ap.parse_args()
-    path = scenes.glass_sphere() if a.scene == "glass" else scenes.cornell()
+    if a.scene == "c4":
+        path = scenes.c4_teapot(env_size=(a.env, a.env // 2))
+        if a.flat:
+            js = json.load(open(path))
+            mat = js["meshes"][1]["material"]
+            for k in a.flat.split(","):
+                if k == "normal":
+                    mat.pop("normal")
+                else:
+                    mat[k] = [0.5, 0.4, 0.3] if k == "rho_d" else 0.3
+            json.dump(js, open(path, "w"))
+    else:
+        path = scenes.glass_sphere() if a.scene == "glass" else scenes.cornell()
     scene = nart_amd.Scene(path)
     p = nart_amd.load_sessions(path)[0]
     p.image_width, p.image_height, p.spp = a.w, a.H, a.s
