@@ -2383,6 +2383,9 @@ __global__ __launch_bounds__(256) void k_splat_skew(SplatArgs A) {
         // (ys_k = yb + k exactly), so every row is hit iff row 0 passes the first and row W-1 the
         // second -- all but never fails (a sample exactly on a pixel edge): the rows then accumulate
         // without per-row branches (4-5 scalar exec-mask instructions and two compares per row).
+        // (A wave-uniform form of this test -- a ballot, the per-row path for the whole wave when any
+        // lane misses a row -- measured slower: C5 splat 69.4-70.5 vs 68.2-68.8 ms,
+        // profiles/r05r_skew_uniform_ab.log.)
         if (xhit && loy < ys[1] && ys[W - 1] < hiy) {
 #pragma unroll
             for (int k = 0; k < W; ++k) {

@@ -179,6 +179,10 @@ ND bool trav_pop1(Trav& t, const int* sc, const float* st, int stride) {
 // One step: descend to the next leaf, test all its triangles, pop the next subtree.  Returns
 // true when the query is resolved (t.bestG = winner or NO_HIT).  (A one-node-or-one-triangle
 // "if-if" step measured slower on C3: 123 vs 95 ms per frame in the wavefront trace kernel.)
+#ifndef NART_TRI_PF
+#define NART_TRI_PF 2  // triangle records loaded per group in the leaf loop (0: one at a time)
+#endif
+#define NART_TRI_PAD 3  // padding records after tri_perm (a group of up to 4 may read past a leaf)
 template <bool COUNT>
 ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, int stride, TraceCounters& cnt,
                   const float4* lnodes, int nl) {
@@ -290,12 +294,11 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
     // without 18 per-triangle selects (C3 at 64 spp: 134.9 -> 133.3 ms).
     const f3 op = permute(r.o, r.major);
     const float4* tpp = S.tri_perm + 4 * ((size_t)r.major * S.num_leaf_tris + first);
-    for (uint32_t i = 0; i < count; ++i) {
+    // one triangle test (geometry.cpp:32-115 through the octree's rules, octree.h); true when an
+    // any-hit query is answered
+    auto test = [&](const float4 b, const float4 c, const float4 dd, const float4 a) -> bool {
         if (COUNT) cnt.tris++;
         if (COUNT) WPROF(cnt, 4);
-        // the plane is loaded with the vertices (same 64-B record), not after the edge test:
-        // one memory round trip per test instead of two
-        const float4 b = tpp[4 * i], c = tpp[4 * i + 1], dd = tpp[4 * i + 2], a = tpp[4 * i + 3];
         f3 p0 = F3(b.x - op.x, b.y - op.y, b.z - op.z);
         f3 p1 = F3(b.w - op.x, c.x - op.y, c.y - op.z);
         f3 p2 = F3(c.z - op.x, c.w - op.y, dd.x - op.z);
@@ -308,12 +311,12 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
         const float e0 = (p1.x * p2.y) - (p1.y * p2.x);
         const float e1 = (p2.x * p0.y) - (p2.y * p0.x);
         const float e2 = (p0.x * p1.y) - (p0.y * p1.x);
-        if (!edges_accept(e0, e1, e2)) continue;
+        if (!edges_accept(e0, e1, e2)) return false;
         f3 n = F3(a.x, a.y, a.z);
         const float den = dot(r.d, n);
         float tt = (a.w - dot(r.o, n)) / den;
-        if (tt != tt) t.risky = true;                   // NaN passes geometry.cpp:37-39 (octree.h)
-        if (!(tt > 0.f) || !(tt < t.tmax)) continue;  // geometry.cpp:37-39 with tMin = 0
+        if (tt != tt) t.risky = true;                       // NaN passes geometry.cpp:37-39 (octree.h)
+        if (!(tt > 0.f) || !(tt < t.tmax)) return false;  // geometry.cpp:37-39 with tMin = 0
         uint32_t g = __float_as_uint(dd.y);
         const uint32_t info = __float_as_uint(dd.z) & (fabsf(den) >= dd.w ? 0xFFFFFFFFu : 0x7FFFFFFFu);
         if (t.any) {
@@ -336,7 +339,32 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
             }
             t.t2 = fminf(t.t2, tt);
         }
+        return false;
+    };
+    // The plane is loaded with the vertices (same 64-B record), not after the edge test: one memory
+    // round trip per record instead of two.
+#if NART_TRI_PF
+    // Records are loaded NART_TRI_PF at a time, all before the first of them is tested (tri_perm
+    // carries padding records, so a leaf's last group may read past it): one memory round trip
+    // per group of tests instead of one per test.
+    constexpr uint32_t K = NART_TRI_PF;
+    for (uint32_t i = 0; i < count; i += K) {
+        float4 rb[K], rc[K], rd[K], ra[K];
+#pragma unroll
+        for (uint32_t u = 0; u < K; ++u) {
+            rb[u] = tpp[4 * (i + u)];
+            rc[u] = tpp[4 * (i + u) + 1];
+            rd[u] = tpp[4 * (i + u) + 2];
+            ra[u] = tpp[4 * (i + u) + 3];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < K; ++u)
+            if ((u == 0 || i + u < count) && test(rb[u], rc[u], rd[u], ra[u])) return true;
     }
+#else
+    for (uint32_t i = 0; i < count; ++i)
+        if (test(tpp[4 * i], tpp[4 * i + 1], tpp[4 * i + 2], tpp[4 * i + 3])) return true;
+#endif
     return !trav_pop1(t, sc, st, stride);
 }
 

@@ -1547,7 +1547,7 @@ int build_bvh_device(nart_ctx* ctx, const nart_scene_blob& blob, const std::vect
     }
     if ((rc = dmalloc(ctx, &ctx->d_nodes, ni * sizeof(BVHNode), "BVH nodes")) ||
         (rc = dmalloc(ctx, &ctx->d_tri_isect, (size_t)m * 64, "triangle records")) ||
-        (rc = dmalloc(ctx, &ctx->d_tri_perm, (size_t)m * 64 * 3, "permuted triangle records")))
+        (rc = dmalloc(ctx, &ctx->d_tri_perm, ((size_t)m * 3 + NART_TRI_PAD) * 64, "permuted triangle records")))
         return cleanup(rc);
     if (ninner > 0)
         hipLaunchKernelGGL(k_lbvh_emit, dim3(gi), blk, 0, 0, d_ord[0], ninner, d_child, d_remap, d_box, d_sorted, m, pad,
@@ -1643,7 +1643,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
         // vertex block of every triangle test record, permuted for each ray major axis, followed
         // by the plane {n, dot(v0, n)}: one 64-B record, so a test issues its four loads at once
         const size_t nt = bvh.tri_isect.size() / 16;
-        std::vector<float> perm(3 * nt * 16);
+        std::vector<float> perm((3 * nt + NART_TRI_PAD) * 16);  // + padding records (trav_step's record groups)
         for (int m = 0; m < 3; ++m) {
             const int kx = (m + 1) % 3, ky = (m + 2) % 3, kz = m;
             for (size_t i = 0; i < nt; ++i) {
