@@ -1,0 +1,12 @@
+#!/bin/bash
+# round 5 checkpoint 2, part 2: the four bench lines (reading profiles/pmc_latest_<config>.json of
+# r05w) and per-rank shard timings of C3 / C5 / C4 at 1/2/4/8 ranks
+step() { tools/gpu_step.sh "$@" || exit 1; }
+step r05x_bench 300 python -u bench.py
+step r05x_bench_c2 300 python -u bench.py --config c2
+step r05x_bench_c5 300 python -u bench.py --config c5
+step r05x_bench_c4 400 python -u bench.py --config c4 --steps 2
+step r05x_shard_c3 300 python -u tools/shard_perf.py --config c3 --ns 1 2 4 8 --reps 2
+step r05x_shard_c5 300 python -u tools/shard_perf.py --config c5 --ns 1 2 4 8 --reps 2
+step r05x_shard_c4 500 python -u tools/shard_perf.py --config c4 --ns 1 2 4 8 --reps 1
+echo all-done
