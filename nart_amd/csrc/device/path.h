@@ -401,6 +401,9 @@ ND bool traverse(const DScene& S, const Ray& r, float tmax, bool ANY, float& bes
 // hit and risky flags the same ties and NaNs or more -- so oc_resolve returns the reference octree's
 // answer as after traverse() (path.h trav_step, octree.h).  wstk: this wave's LDS stack, 16 B per
 // level.
+#ifndef NART_PACKET_SLOAD
+#define NART_PACKET_SLOAD 1
+#endif
 template <bool COUNT>
 ND void traverse_packet(const DScene& S, const Ray& r, float tmax, float& bestT, uint32_t& bestG, uint4* wstk,
                         TraceCounters& cnt) {
@@ -414,13 +417,29 @@ ND void traverse_packet(const DScene& S, const Ray& r, float tmax, float& bestT,
     uint64_t mask = __ballot(1);
     int sp = 0;
     const f3 op = permute(r.o, r.major);
+#if NART_PACKET_SLOAD
+    const int maj0 = __builtin_amdgcn_readfirstlane(r.major);
+    const bool umaj = __ballot(r.major != maj0) == 0;
+#endif
     for (;;) {
         const bool in = (mask >> me) & 1ull;
         bool pop = false;
         if (code >= 0) {
+#if NART_PACKET_SLOAD
+            // code is wave-uniform: the node is read through the constant address space, i.e. as
+            // one scalar load (the node array is not written while a render kernel runs)
+            typedef float v4f __attribute__((ext_vector_type(4)));
+            typedef const __attribute__((address_space(4))) v4f c_v4f;
+            const c_v4f* np = (const c_v4f*)(uintptr_t)(S.nodes + code);
+            const v4f qa = np[0], qb = np[1], qc = np[2], qk = np[3];
+            const float4 a = make_float4(qa.x, qa.y, qa.z, qa.w), b = make_float4(qb.x, qb.y, qb.z, qb.w),
+                         c = make_float4(qc.x, qc.y, qc.z, qc.w);
+            const int4 k = make_int4(__float_as_int(qk.x), __float_as_int(qk.y), __float_as_int(qk.z), __float_as_int(qk.w));
+#else
             const float4* np = reinterpret_cast<const float4*>(S.nodes + code);
             const float4 a = np[0], b = np[1], c = np[2];
             const int4 k = reinterpret_cast<const int4*>(np)[3];
+#endif
             const f3 inv = t.inv, oi = t.oi;
             const float tx0 = fmaf(a.x, inv.x, oi.x), tx1 = fmaf(a.w, inv.x, oi.x);
             const float ty0 = fmaf(a.y, inv.y, oi.y), ty1 = fmaf(b.x, inv.y, oi.y);
@@ -465,7 +484,26 @@ ND void traverse_packet(const DScene& S, const Ray& r, float tmax, float& bestT,
                 // profiles/r05u_packet_pairs_ab.log)
                 for (uint32_t i = 0; i < count; ++i) {
                     if (COUNT) cnt.tris++;
+#if NART_PACKET_SLOAD
+                    float4 tb, tc, dd, ta;
+                    if (umaj) {  // every ray of the wave has this major axis: one scalar load
+                        typedef float v4f __attribute__((ext_vector_type(4)));
+                        typedef const __attribute__((address_space(4))) v4f c_v4f;
+                        const c_v4f* q = (const c_v4f*)(uintptr_t)(S.tri_perm + 4 * ((size_t)maj0 * S.num_leaf_tris + first + i));
+                        const v4f q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+                        tb = make_float4(q0.x, q0.y, q0.z, q0.w);
+                        tc = make_float4(q1.x, q1.y, q1.z, q1.w);
+                        dd = make_float4(q2.x, q2.y, q2.z, q2.w);
+                        ta = make_float4(q3.x, q3.y, q3.z, q3.w);
+                    } else {
+                        tb = tpp[4 * i];
+                        tc = tpp[4 * i + 1];
+                        dd = tpp[4 * i + 2];
+                        ta = tpp[4 * i + 3];
+                    }
+#else
                     const float4 tb = tpp[4 * i], tc = tpp[4 * i + 1], dd = tpp[4 * i + 2], ta = tpp[4 * i + 3];
+#endif
                     f3 p0 = F3(tb.x - op.x, tb.y - op.y, tb.z - op.z);
                     f3 p1 = F3(tb.w - op.x, tc.x - op.y, tc.y - op.z);
                     f3 p2 = F3(tc.z - op.x, tc.w - op.y, dd.x - op.z);
