@@ -11,7 +11,7 @@ namespace nd {
 // TexturePattern::Pdf / ConstantPattern::Pdf of the env light's Le (texturepattern.cpp:160-170)
 ND float env_ptn_pdf(const DScene& S, const DLight& L, f2 st) {
     if (L.Le.type == NART_PTN_CONSTANT || L.env < 0) return 1.f;
-    return env_pdf(S.envs[L.env], F2(gmin(st.x, 0.9999f), gmin(st.y, 0.9999f)));
+    return env_pdf(cst(S.envs)[L.env], F2(gmin(st.x, 0.9999f), gmin(st.y, 0.9999f)));
 }
 
 // Light::Li (disklight.cpp:12-23, ringlight.cpp:13-24, environmentlight.cpp:9-28).
@@ -43,6 +43,10 @@ ND f3 light_li(const DScene& S, const DLight& L, f3 p, f3 wi, float* pdf, float&
     return F3(0.f, 0.f, 0.f);
 }
 
+// A light record at a wave-uniform index (the light loops' j), read through the constant address
+// space (cst, dscene.h): the compiler then reads its fields with scalar loads.
+ND const DLight& uniform_light(const DScene& S, uint32_t j) { return cst(S.lights)[j]; }
+
 // The light loop of an extension ray (pathintegrator.cpp:171-182) when its Le cannot reach L: Le
 // is used only when the camera ray escapes (pathintegrator.cpp:252-256, Q7), so for every other
 // ray the loop needs just the bound tMax (and whether it was lowered), which this sets exactly as
@@ -70,7 +74,7 @@ ND f3 light_sample_li(const DScene& S, const DLight& L, f3 p, f3& wi, f2 sample,
             Lv = F3(L.Le.v[0], L.Le.v[1], L.Le.v[2]);
         } else {
             if (L.env < 0) pdf = 1.f;
-            else ps = env_sample(S.envs[L.env], sample, pdf);  // leaves pdf as is on a zero row
+            else ps = env_sample(cst(S.envs)[L.env], sample, pdf);  // leaves pdf as is on a zero row
             Lv = tex_fetch(S, L.Le.tex, ps.x, ps.y, L.Le.rough);
         }
         Lv = muls(Lv, L.intensity);

@@ -727,7 +727,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
             uint32_t lwin = 0;
             for (uint32_t j = 0; j < S.num_lights; ++j) {
                 float lt = __builtin_inff();
-                light_bound<ENV>(S.lights[j], ray.o, ray.d, lt);
+                light_bound<ENV>(uniform_light(S, j), ray.o, ray.d, lt);
                 if (lt < lightTMax) {
                     lightTMax = lt;
                     lightHit = true;
@@ -738,7 +738,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
             // Le (the radiance of the light that set the bound) only matters for the camera ray
             if (bounce == 0 && lightHit) {
                 float lt = __builtin_inff();
-                Le = light_li<ENV>(S, S.lights[lwin], ray.o, ray.d, nullptr, lt);
+                Le = light_li<ENV>(S, cst(S.lights)[lwin], ray.o, ray.d, nullptr, lt);
             }
             cur = ray;
             tmax = lightTMax;
@@ -799,7 +799,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
                 SECT(3, st0);
                 st0 = SECT_T();
                 // ---- EstimateDirect (pathintegrator.cpp:38-121)
-                const DLight& Lg = S.lights[f2u8(gmin(rng_float(rng), ND_ONE_MINUS_EPS) * nL)];
+                const DLight& Lg = cst(S.lights)[f2u8(gmin(rng_float(rng), ND_ONE_MINUS_EPS) * nL)];
                 float sPdf = 0.f, lPdf = 0.f;
                 float sx = rng_float(rng);
                 float sy = rng_float(rng);
@@ -996,7 +996,7 @@ __global__ __launch_bounds__(256) void k_primary(DScene S, RenderArgs A, uint32_
         float lightTMax = __builtin_inff();
         for (uint32_t j = 0; j < S.num_lights; ++j) {
             float lt = __builtin_inff();
-            light_bound<ENV>(S.lights[j], ray.o, ray.d, lt);  // only the bound: no radiance
+            light_bound<ENV>(uniform_light(S, j), ray.o, ray.d, lt);  // only the bound: no radiance
             if (lt < lightTMax) lightTMax = lt;
         }
         float bt;
@@ -1254,7 +1254,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
         lightHit = false;
         for (uint32_t j = 0; j < S.num_lights; ++j) {
             float lt = __builtin_inff();
-            light_bound<ENV>(S.lights[j], o, d, lt);
+            light_bound<ENV>(uniform_light(S, j), o, d, lt);
             if (lt < lightTMax) {
                 lightTMax = lt;
                 lightHit = true;
@@ -1266,7 +1266,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
     };
     auto light_le = [&](f3 o, f3 d) {
         float lt = __builtin_inff();
-        return light_li<ENV>(S, S.lights[lwin], o, d, nullptr, lt);
+        return light_li<ENV>(S, cst(S.lights)[lwin], o, d, nullptr, lt);
     };
     auto draw = [&]() {
         ++nd;
@@ -1629,7 +1629,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
                 if (bounce == 0) alpha = 1.f;
                 const f3 wo = to_local(bsdf, neg(cur.d));
                 // ---- EstimateDirect (pathintegrator.cpp:38-121)
-                const DLight& Lg = S.lights[f2u8(gmin(draw(), ND_ONE_MINUS_EPS) * nL)];
+                const DLight& Lg = cst(S.lights)[f2u8(gmin(draw(), ND_ONE_MINUS_EPS) * nL)];
                 float sPdf = 0.f, lPdf = 0.f;
                 float sx = draw();
                 float sy = draw();

@@ -584,8 +584,8 @@ ND void fill_isect(const DScene& S, const Ray& r, uint32_t g, Isect& is) {
     is.dpdt = muls(add(muls(sub(v0, v2), T.uv2[0] - T.uv1[0]), muls(sub(v1, v2), T.uv0[0] - T.uv2[0])), invUVDet);
     uint32_t mesh = S.tri_mesh[g];
     is.meshID = mesh;
-    is.priority = S.meshes[mesh].priority;
-    is.mat = S.meshes[mesh].material;
+    is.priority = cst(S.meshes)[mesh].priority;
+    is.mat = cst(S.meshes)[mesh].material;
 }
 
 // ---------------------------------------------------------------- patterns
@@ -605,7 +605,7 @@ ND float half_to_float(uint16_t h) {  // Imath half -> float (exact)
     return __uint_as_float(v);
 }
 ND f3 tex_fetch(const DScene& S, int tex, float su, float sv, int rough) {  // texturepattern.cpp:172-187
-    const DTexture& t = S.texs[tex];
+    const DTexture& t = cst(S.texs)[tex];
     float u = gmin(gmax(su, 0.0001f), 0.9999f);
     float v = gmin(gmax(1.f - sv, 0.0001f), 0.9999f);
     int iu = (int)((float)t.w * u);
@@ -1046,7 +1046,7 @@ ND float bsdf_sample_eta(const BSDF& s, float s1) { return bxdf_eta(s.b[f2u8(s1 
 
 // Material::CreateBSDF (src/materials/*.cpp)
 ND void create_bsdf(const DScene& S, const Isect& is, float alphaTweak, BSDF& bs) {
-    const DMaterial& m = S.mats[is.mat];
+    const DMaterial& m = cst(S.mats)[is.mat];
     bs.n = is.sn;
     bs.num = m.type == NART_MAT_PLASTIC ? 2u : 1u;
     if (m.has_normal) {

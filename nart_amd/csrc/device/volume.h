@@ -258,7 +258,7 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
             f3 Le = F3(0.f, 0.f, 0.f);
             for (uint32_t j = 0; j < S.num_lights; ++j) {
                 float lt = __builtin_inff();
-                const f3 Li = light_li(S, S.lights[j], o, d, nullptr, lt, theta);
+                const f3 Li = light_li(S, uniform_light(S, j), o, d, nullptr, lt, theta);
                 if (lt < lightTMax) {
                     Le = Li;
                     lightTMax = lt;

@@ -36,6 +36,8 @@ def main():
                 else:
                     mat[k] = [0.5, 0.4, 0.3] if k == "rho_d" else 0.3
             json.dump(js, open(path, "w"))
+    elif a.scene == "c5":
+        path = scenes.volume(width=a.w, height=a.H, spp=a.s, kind="c5")
     else:
         path = scenes.glass_sphere() if a.scene == "glass" else scenes.cornell()
     scene = nart_amd.Scene(path)
