@@ -178,6 +178,9 @@ ND bool maj_next(const DMedium& m, MajIter& it, float& sigma, float& t0, float& 
 // exactly the reference's RNG draws and float operations in its order: bit-identical.
 // WV: minimum waves per SIMD requested from the register allocator (dispatch_volume: 4 on
 // throughput-bound launches, 1 on small shards)
+#ifndef NART_VOL_WV
+#define NART_VOL_WV 4  // waves per SIMD of the throughput-bound launches (dispatch_volume)
+#endif
 #ifndef NART_VOL_PREFETCH
 #define NART_VOL_PREFETCH 1
 #endif

@@ -954,7 +954,7 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
         }
     }
     if (ctx->counters) hipLaunchKernelGGL((k_render_volume_sm<true, 1>), dim3(grid), block, dl, st, ctx->scene, b);
-    else if (w4) hipLaunchKernelGGL((k_render_volume_sm<false, 4>), dim3(grid), block, dl, st, ctx->scene, b);
+    else if (w4) hipLaunchKernelGGL((k_render_volume_sm<false, NART_VOL_WV>), dim3(grid), block, dl, st, ctx->scene, b);
     else hipLaunchKernelGGL((k_render_volume_sm<false, 1>), dim3(grid), block, dl, st, ctx->scene, b);
     HIPCHK(hipGetLastError());
     return NART_OK;
