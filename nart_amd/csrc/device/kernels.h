@@ -524,11 +524,24 @@ ND float latin_value(uint32_t k, uint32_t y, float inv) {
 #ifndef LATIN_EMIT_U
 #define LATIN_EMIT_U 8
 #endif
+#ifndef NART_LATIN_XCD
+#define NART_LATIN_XCD 1
+#endif
 __global__ __launch_bounds__(256) void k_latin_emit(RenderArgs A, LatinScratch L) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_st[];  // [k][p]
     constexpr uint32_t P = LATIN_EMIT_SLOTS, RS = 256 / P, U = LATIN_EMIT_U;
     const uint32_t n = A.spp, n2 = L.n2, t = threadIdx.x, p = t % P;
-    const uint32_t slot = blockIdx.x * P + p;
+#if NART_LATIN_XCD
+    // XCD-aware block order: the four blocks whose 16 slots share the 256-B rows of one 64-slot
+    // index group are consecutive logical blocks on one XCD (blocks are dealt round robin over the
+    // 8 XCDs, each with its own L2), so each row is fetched once instead of once per quarter.
+    // Bijective for any grid (cdna_hip_programming.md T1).
+    const uint32_t nwg = gridDim.x, q = nwg / 8u, r = nwg % 8u, x = blockIdx.x % 8u;
+    const uint32_t bid = (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + blockIdx.x / 8u;
+#else
+    const uint32_t bid = blockIdx.x;
+#endif
+    const uint32_t slot = bid * P + p;
     const bool live = slot < A.n_slots;
     const uint32_t* sx = L.sx + latin_row(slot >> 6, n2, 0, slot & 63u);
     const uint32_t* sy = L.sy + latin_row(slot >> 6, n2, 0, slot & 63u);
@@ -543,7 +556,7 @@ __global__ __launch_bounds__(256) void k_latin_emit(RenderArgs A, LatinScratch L
     // stage the block's n*P states: 8 unconditional 16-B loads in flight per thread (the st
     // region carries LATIN_ST_PAD words of padding), guarded LDS stores
     {
-        const uint4* src = reinterpret_cast<const uint4*>(L.st + (size_t)blockIdx.x * n * P);
+        const uint4* src = reinterpret_cast<const uint4*>(L.st + (size_t)bid * n * P);
         uint4* dst = reinterpret_cast<uint4*>(s_st);
         const uint32_t cnt = n * P / 4;
         for (uint32_t b0 = 0; b0 < cnt; b0 += 256u * 8u) {
