@@ -137,6 +137,8 @@ struct RenderArgs {
     uint32_t* qhead = nullptr;
     uint32_t qbase = 0;
     uint32_t* cost = nullptr; // cost probe: per-slot work estimate of the rendered sample(s)
+    uint32_t probe_sub = 0;   // cost probe of wave groups: probe this many pixels per 64-slot
+                              // group (lane gid -> group gid / probe_sub), 0: every slot
     uint32_t rq_quorum = 8;   // k_render_rq: leave a traversal phase once the wave's queue is empty
                               // and at most this many lanes still trace
     const uint32_t* prim = nullptr;  // k_render_rq: camera-ray hits from k_primary, same indexing as samples
@@ -635,7 +637,11 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
     const int tid = threadIdx.x;
     const uint32_t gid = blockIdx.x * blockDim.x + tid;
     uint32_t slot = gid;
-    if (A.queue) {
+    if (A.probe_sub) {  // evenly spaced pixels of each 64-slot group
+        const uint32_t q = A.probe_sub;
+        slot = (gid / q) * 64u + (gid % q) * (64u / q) + (32u / q);
+        if (slot >= A.n_slots) return;
+    } else if (A.queue) {
         slot = gid < A.n_slots ? A.queue[gid] : 0xFFFFFFFFu;
     } else if (slot >= A.n_slots) {
         return;

@@ -485,13 +485,19 @@ bool rq_fits(const nart_ctx* ctx) {
 
 // Group (wave-sized run of 64 consecutive slots: a 16x4 strip of a bucket) costs, as keys of an
 // ascending sort that puts the costliest group first; a partial last group always sorts last.
-__global__ void k_group_keys(const uint32_t* cost, uint32_t n, uint32_t* keys, uint32_t* vals) {
+// per: cost entries per group (64: one per slot; fewer: the sampled probe, probe_sub).
+__global__ void k_group_keys(const uint32_t* cost, uint32_t n, uint32_t* keys, uint32_t* vals, uint32_t per = 64) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t ng = (n + 63) / 64;
     if (g >= ng) return;
     uint64_t sum = 0;
     const uint32_t e = min(n, 64 * g + 64);
-    for (uint32_t i = 64 * g; i < e; ++i) sum += cost[i];
+    if (per < 64) {  // a partial last group is keyed last below, whatever its entries hold
+        if (e - 64 * g == 64)
+            for (uint32_t i = per * g; i < per * g + per; ++i) sum += cost[i];
+    } else {
+        for (uint32_t i = 64 * g; i < e; ++i) sum += cost[i];
+    }
     const uint32_t c = (uint32_t)min<uint64_t>(sum, 0xFFFFFFFEull);
     keys[g] = (e - 64 * g < 64) ? 0xFFFFFFFFu : 0xFFFFFFFEu - c;
     vals[g] = g;
@@ -754,14 +760,23 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
                     const int order = std::getenv("NART_RQ_ORDER") ? std::atoi(std::getenv("NART_RQ_ORDER")) : 2;
                     ctx->sched |= NART_SCHED_WAVE_GROUPS;
                     if (order == 1 || order == 2) {
-                        RenderArgs pb = b;  // cost probe: the first sample of every pixel
+                        // cost probe: the first sample of NART_PROBE_SUB (default 8) evenly spaced
+                        // pixels of every 64-slot group (64: every pixel).  Only the group order
+                        // depends on it (costliest NART_RQ_TOPF % first), and that order is not
+                        // sensitive to the estimate (TOPF 10 / 20 / 35 %: 407 / 408 / 408 ms)
+                        const uint32_t ng = (n + 63) / 64;
+                        uint32_t sub = std::getenv("NART_PROBE_SUB") ? (uint32_t)std::atoi(std::getenv("NART_PROBE_SUB")) : 8u;
+                        if (sub != 1u && sub != 2u && sub != 4u && sub != 8u && sub != 16u && sub != 32u) sub = 64u;
+                        RenderArgs pb = b;
                         pb.spp = 1;
                         pb.cost = ctx->d_cost;
                         pb.ghead = nullptr;
-                        hipLaunchKernelGGL((k_render<EXT, true, ENV>), dim3(blocks), block, lds, st, ctx->scene, pb);
-                        const uint32_t ng = (n + 63) / 64;
+                        pb.probe_sub = sub < 64u ? sub : 0u;
+                        const uint32_t pblocks = sub < 64u ? (ng * sub + 255u) / 256u : blocks;
+                        hipLaunchKernelGGL((k_render<EXT, true, ENV>), dim3(pblocks), block, lds, st, ctx->scene, pb);
                         const dim3 gg((ng + 255) / 256);
-                        hipLaunchKernelGGL(k_group_keys, gg, block, 0, st, ctx->d_cost, n, ctx->d_keys[0], ctx->d_vals[0]);
+                        hipLaunchKernelGGL(k_group_keys, gg, block, 0, st, ctx->d_cost, n, ctx->d_keys[0], ctx->d_vals[0],
+                                           sub);
                         size_t tmp = ctx->cap_sort_tmp;
                         HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->d_sort_tmp, tmp, ctx->d_keys[0], ctx->d_keys[1],
                                                                   ctx->d_vals[0], ctx->d_vals[1], (int)ng, 0, 32, st));
