@@ -185,9 +185,12 @@ ND size_t sample_index(const RenderArgs& A, uint32_t slot, uint32_t s) {
 }
 
 // Stage the top BVH nodes (breadth-first prefix) into LDS; every thread of the block calls it.
+// With NART_NODE_SWZ the 16-B quarter k of node i sits at quarter (k + (i >> 2)) & 3 of the node's
+// 64 B (node_quarter, path.h), so that the 16-lane groups of a ds_read_b128 spread over all 16
+// bank slots of a 256-B LDS row instead of the 4 that node i mod 4 selects.
 ND void stage_nodes(const DScene& S, float4* dst, uint32_t n) {
     const float4* src = reinterpret_cast<const float4*>(S.nodes);
-    for (uint32_t i = threadIdx.x; i < 4 * n; i += blockDim.x) dst[i] = src[i];
+    for (uint32_t i = threadIdx.x; i < 4 * n; i += blockDim.x) dst[(i & ~3u) | node_quarter(i >> 2, i & 3u)] = src[i];
     __syncthreads();
 }
 

@@ -179,6 +179,19 @@ ND bool trav_pop1(Trav& t, const int* sc, const float* st, int stride) {
 // One step: descend to the next leaf, test all its triangles, pop the next subtree.  Returns
 // true when the query is resolved (t.bestG = winner or NO_HIT).  (A one-node-or-one-triangle
 // "if-if" step measured slower on C3: 123 vs 95 ms per frame in the wavefront trace kernel.)
+#ifndef NART_NODE_SWZ
+// 1: rotate the quarters of LDS-staged nodes (bank spread): C4 path kernel 52.1 -> 51.3 ms but C3
+// 276.2 -> 279.4 ms (the per-visit address arithmetic), profiles/r05ad_node_swz_ab.txt
+#define NART_NODE_SWZ 0
+#endif
+// LDS quarter of 16-B part k of BVH node i (stage_nodes, kernels.h)
+NHD inline uint32_t node_quarter(uint32_t i, uint32_t k) {
+#if NART_NODE_SWZ
+    return (k + (i >> 2)) & 3u;
+#else
+    return k;
+#endif
+}
 #ifndef NART_TRI_PF
 #define NART_TRI_PF 2  // triangle records loaded per group in the leaf loop (0: one at a time)
 #endif
@@ -199,7 +212,8 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
             typedef float v4f __attribute__((ext_vector_type(4)));
             typedef const __attribute__((address_space(3))) v4f lds_v4f;
             lds_v4f* np = (lds_v4f*)lnodes + 4 * t.code;
-            const v4f qa = np[0], qb = np[1], qc = np[2], qk = np[3];
+            const uint32_t r = node_quarter((uint32_t)t.code, 0u);
+            const v4f qa = np[r], qb = np[(r + 1u) & 3u], qc = np[(r + 2u) & 3u], qk = np[(r + 3u) & 3u];
             a = make_float4(qa.x, qa.y, qa.z, qa.w);
             b = make_float4(qb.x, qb.y, qb.z, qb.w);
             c = make_float4(qc.x, qc.y, qc.z, qc.w);
@@ -217,17 +231,19 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
             typedef float v4f __attribute__((ext_vector_type(4)));
             typedef const __attribute__((address_space(3))) v4f lds_v4f;
             lds_v4f* np = (lds_v4f*)lnodes + 4 * t.code;
-            const v4f qa = np[0], qb = np[1], qc = np[2], qk = np[3];
+            const uint32_t r = node_quarter((uint32_t)t.code, 0u);
+            const v4f qa = np[r], qb = np[(r + 1u) & 3u], qc = np[(r + 2u) & 3u], qk = np[(r + 3u) & 3u];
             a = make_float4(qa.x, qa.y, qa.z, qa.w);
             b = make_float4(qb.x, qb.y, qb.z, qb.w);
             c = make_float4(qc.x, qc.y, qc.z, qc.w);
             k = make_int4(__float_as_int(qk.x), __float_as_int(qk.y), __float_as_int(qk.z), __float_as_int(qk.w));
 #else
             const float4* np = lnodes + 4 * t.code;
-            a = np[0];
-            b = np[1];
-            c = np[2];
-            k = reinterpret_cast<const int4*>(np)[3];
+            const uint32_t r = node_quarter((uint32_t)t.code, 0u);
+            a = np[r];
+            b = np[(r + 1u) & 3u];
+            c = np[(r + 2u) & 3u];
+            k = reinterpret_cast<const int4*>(np)[(r + 3u) & 3u];
 #endif
         } else {
             const float4* np = reinterpret_cast<const float4*>(S.nodes + t.code);
