@@ -190,7 +190,7 @@ ND size_t sample_index(const RenderArgs& A, uint32_t slot, uint32_t s) {
 // bank slots of a 256-B LDS row instead of the 4 that node i mod 4 selects.
 ND void stage_nodes(const DScene& S, float4* dst, uint32_t n) {
     const float4* src = reinterpret_cast<const float4*>(S.nodes);
-    for (uint32_t i = threadIdx.x; i < 4 * n; i += blockDim.x) dst[(i & ~3u) | node_quarter(i >> 2, i & 3u)] = src[i];
+    for (uint32_t i = threadIdx.x; i < 4 * n; i += blockDim.x) dst[node_slot(i >> 2) + node_quarter(i >> 2, i & 3u)] = src[i];
     __syncthreads();
 }
 

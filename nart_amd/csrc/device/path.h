@@ -184,6 +184,22 @@ ND bool trav_pop1(Trav& t, const int* sc, const float* st, int stride) {
 // 276.2 -> 279.4 ms (the per-visit address arithmetic), profiles/r05ad_node_swz_ab.txt
 #define NART_NODE_SWZ 0
 #endif
+#ifndef NART_NODE_PAD
+// 1: measured C3 path kernel 276.3 -> 282.5 ms, C4 51.9 -> 51.6 ms (profiles/r05ae_node_pad_ab.txt)
+#define NART_NODE_PAD 0
+#endif
+// LDS-staged nodes: with NART_NODE_PAD a 16-B pad follows every 4 nodes, so that node i starts at
+// 16-B slot (5 i / 4 + ...) mod 16 of a 256-B LDS row: the 16-lane groups of a ds_read_b128 of
+// random nodes spread over all 16 slots instead of the 4 that i mod 4 selects (bank conflicts),
+// for one extra shift-and-add per node visit.  node_slot: first float4 of node i.
+NHD inline uint32_t node_slot(uint32_t i) {
+#if NART_NODE_PAD
+    return 4u * i + (i >> 2);
+#else
+    return 4u * i;
+#endif
+}
+NHD inline size_t node_lds_bytes(uint32_t n) { return (size_t)16 * (n ? node_slot(n - 1u) + 4u : 0u); }
 // LDS quarter of 16-B part k of BVH node i (stage_nodes, kernels.h)
 NHD inline uint32_t node_quarter(uint32_t i, uint32_t k) {
 #if NART_NODE_SWZ
@@ -211,7 +227,7 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
         if (true) {
             typedef float v4f __attribute__((ext_vector_type(4)));
             typedef const __attribute__((address_space(3))) v4f lds_v4f;
-            lds_v4f* np = (lds_v4f*)lnodes + 4 * t.code;
+            lds_v4f* np = (lds_v4f*)lnodes + node_slot((uint32_t)t.code);
             const uint32_t r = node_quarter((uint32_t)t.code, 0u);
             const v4f qa = np[r], qb = np[(r + 1u) & 3u], qc = np[(r + 2u) & 3u], qk = np[(r + 3u) & 3u];
             a = make_float4(qa.x, qa.y, qa.z, qa.w);
@@ -230,7 +246,7 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
             // 577 vs 570 ms the other way).  -DNART_NODE_FLAT restores the flat load.
             typedef float v4f __attribute__((ext_vector_type(4)));
             typedef const __attribute__((address_space(3))) v4f lds_v4f;
-            lds_v4f* np = (lds_v4f*)lnodes + 4 * t.code;
+            lds_v4f* np = (lds_v4f*)lnodes + node_slot((uint32_t)t.code);
             const uint32_t r = node_quarter((uint32_t)t.code, 0u);
             const v4f qa = np[r], qb = np[(r + 1u) & 3u], qc = np[(r + 2u) & 3u], qk = np[(r + 3u) & 3u];
             a = make_float4(qa.x, qa.y, qa.z, qa.w);
@@ -238,7 +254,7 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
             c = make_float4(qc.x, qc.y, qc.z, qc.w);
             k = make_int4(__float_as_int(qk.x), __float_as_int(qk.y), __float_as_int(qk.z), __float_as_int(qk.w));
 #else
-            const float4* np = lnodes + 4 * t.code;
+            const float4* np = lnodes + node_slot((uint32_t)t.code);
             const uint32_t r = node_quarter((uint32_t)t.code, 0u);
             a = np[r];
             b = np[(r + 1u) & 3u];

@@ -457,6 +457,7 @@ uint32_t render_lds_nodes(const nart_ctx* ctx, size_t fixed = 0, uint32_t blocks
     const size_t stack = fixed ? fixed : (size_t)ctx->stack_depth * 256 * 8;
     const size_t budget = (size_t)160 * 1024 * blocks_of_256 / NART_RENDER_WAVES;
     size_t n = budget > stack ? (budget - stack) / sizeof(BVHNode) : 0;
+    while (n && node_lds_bytes((uint32_t)n) > budget - stack) --n;  // NART_NODE_PAD padding
     if (const char* e = std::getenv("NART_LDS_NODES")) n = (size_t)std::strtoul(e, nullptr, 10);
     return (uint32_t)std::min<size_t>(n, ctx->num_nodes);
 }
@@ -671,7 +672,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
     const double q_rounds = 3.0;
     RenderArgs b = a;
     b.lds_nodes = render_lds_nodes(ctx);
-    const size_t lds = (size_t)ctx->stack_depth * 256 * 8 + (size_t)b.lds_nodes * sizeof(BVHNode);
+    const size_t lds = (size_t)ctx->stack_depth * 256 * 8 + node_lds_bytes(b.lds_nodes);
     RenderArgs brq = a;  // ray-queue kernel: outbox, results and id lists take part of the LDS
     if (rq && primary && ctx->d_prim && a.cost == nullptr) {
         // (staging the top BVH nodes in LDS, as the path kernel does, measured slower here: a
@@ -692,7 +693,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
         brq.prim = ctx->d_prim;
     }
     brq.lds_nodes = render_lds_nodes(ctx, rq_lds_bytes(ctx->stack_depth, RQB), RQB / 256);
-    const size_t lds_rq = rq_lds_bytes(ctx->stack_depth, RQB) + (size_t)brq.lds_nodes * sizeof(BVHNode);
+    const size_t lds_rq = rq_lds_bytes(ctx->stack_depth, RQB) + node_lds_bytes(brq.lds_nodes);
     const dim3 block(256);
     uint32_t blocks = (a.n_slots + 255) / 256;
     const int mode = queue_mode();
@@ -2025,7 +2026,7 @@ int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t
         r2.rq_pairs = Q;
         r2.rq_quorum = 0;
         r2.lds_nodes = render_lds_nodes(ctx, rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK), NART_RQ_BLOCK / 256);
-        const size_t lds_rq = rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK) + (size_t)r2.lds_nodes * sizeof(BVHNode);
+        const size_t lds_rq = rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK) + node_lds_bytes(r2.lds_nodes);
         static bool attr = false;
         auto kern = k_render_rq<false, false, false>;
         if (!attr) {
