@@ -765,8 +765,15 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
                         // pixels of every 64-slot group (64: every pixel).  Only the group order
                         // depends on it (costliest NART_RQ_TOPF % first), and that order is not
                         // sensitive to the estimate (TOPF 10 / 20 / 35 %: 407 / 408 / 408 ms)
+                        // Launches of fewer than NART_PROBE_SUB_ROUNDS (12) rounds of resident waves
+                        // probe every pixel: there a costly group the sample missed and took late
+                        // sets the tail (C4 1/8 shards, 8 rounds: worst rank 488-496 ms probing every
+                        // pixel, 552-556 ms sampled; profiles/r05ah_c4_probe_ab.log)
                         const uint32_t ng = (n + 63) / 64;
-                        uint32_t sub = std::getenv("NART_PROBE_SUB") ? (uint32_t)std::atoi(std::getenv("NART_PROBE_SUB")) : 8u;
+                        const double sub_rounds =
+                            std::getenv("NART_PROBE_SUB_ROUNDS") ? std::atof(std::getenv("NART_PROBE_SUB_ROUNDS")) : 12.0;
+                        uint32_t sub = std::getenv("NART_PROBE_SUB") ? (uint32_t)std::atoi(std::getenv("NART_PROBE_SUB"))
+                                                                     : (R >= sub_rounds ? 8u : 64u);
                         if (sub != 1u && sub != 2u && sub != 4u && sub != 8u && sub != 16u && sub != 32u) sub = 64u;
                         RenderArgs pb = b;
                         pb.spp = 1;
