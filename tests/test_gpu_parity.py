@@ -148,6 +148,19 @@ def test_group_refill_order(gpu, glass_scene, full_frame_1spp, monkeypatch, orde
     assert _bits_equal(g, r), _report(g, r)
 
 
+@pytest.mark.parametrize("sub", ["1", "8", "64"], ids=["probe-1-per-group", "probe-8-per-group", "probe-every-pixel"])
+def test_group_probe_sampling(gpu, glass_scene, full_frame_1spp, monkeypatch, sub):
+    """The wave-group order's cost probe samples NART_PROBE_SUB pixels of each 64-slot group (8 by
+    default on launches of >= 12 rounds): the estimate only orders the groups, so every setting
+    renders the oracle's frame bit for bit, on the wave-group path."""
+    monkeypatch.setenv("NART_PROBE_SUB", sub)
+    p, r = full_frame_1spp
+    st = nart_amd.RenderStats()
+    g = nart_amd.HipRenderer(glass_scene, variant=0).render(p, st)
+    assert "wave_groups" in st.schedule_names(), st.schedule_names()
+    assert _bits_equal(g, r), _report(g, r)
+
+
 def test_queue_scheduler_environment(gpu, env_scene):
     p = _params(env_scene, 480, 300, 2)
     g = nart_amd.HipRenderer(env_scene, variant=0).render(p)
