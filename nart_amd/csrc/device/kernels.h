@@ -188,9 +188,10 @@ ND size_t sample_index(const RenderArgs& A, uint32_t slot, uint32_t s) {
 // With NART_NODE_SWZ the 16-B quarter k of node i sits at quarter (k + (i >> 2)) & 3 of the node's
 // 64 B (node_quarter, path.h), so that the 16-lane groups of a ds_read_b128 spread over all 16
 // bank slots of a 256-B LDS row instead of the 4 that node i mod 4 selects.
+template <bool ROT = false>
 ND void stage_nodes(const DScene& S, float4* dst, uint32_t n) {
     const float4* src = reinterpret_cast<const float4*>(S.nodes);
-    for (uint32_t i = threadIdx.x; i < 4 * n; i += blockDim.x) dst[node_slot(i >> 2) + node_quarter(i >> 2, i & 3u)] = src[i];
+    for (uint32_t i = threadIdx.x; i < 4 * n; i += blockDim.x) dst[node_slot(i >> 2) + node_quarter<ROT>(i >> 2, i & 3u)] = src[i];
     __syncthreads();
 }
 
@@ -1127,6 +1128,9 @@ NHD size_t rq_lds_bytes(uint32_t stack_depth, uint32_t block) {
 #ifndef NART_RQ_BLOCK
 #define NART_RQ_BLOCK 512
 #endif
+#ifndef NART_NODE_ROT_ENV
+#define NART_NODE_ROT_ENV 1  // the environment-light builds rotate the LDS node quarters (path.h)
+#endif
 // The counter pass (COUNT: untimed, its counts are per ray and do not depend on the schedule) runs
 // 256-lane blocks at one wave per SIMD, so its counters do not push the kernel past 256 VGPRs.
 #define RQ_BLOCK_OF(COUNT) ((COUNT) ? 256 : NART_RQ_BLOCK)
@@ -1143,7 +1147,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
     uint8_t* s_nring = reinterpret_cast<uint8_t*>(s_res + blockDim.x) + wv * 2 * RQ_RING;  // this wave's id rings
     uint8_t* s_pring = s_nring + RQ_RING;
     float4* s_nodes = reinterpret_cast<float4*>(reinterpret_cast<uint8_t*>(s_res + blockDim.x) + nwave * 2 * RQ_RING);
-    stage_nodes(S, s_nodes, A.lds_nodes);
+    stage_nodes<ENV && NART_NODE_ROT_ENV>(S, s_nodes, A.lds_nodes);
     const int nl = (int)A.lds_nodes;
     float4* my_out = s_out + (size_t)wv * 3 * 64 * 2;  // kind k, lane l: my_out[(k * 64 + l) * 2]
     uint4* my_res = s_res + tid;
@@ -1823,7 +1827,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
 #ifdef NART_WAVEPROF
                 const uint32_t pn0 = cnt.nodes, pt0 = cnt.tris;
 #endif
-                if (!fin) fin = trav_step<COUNT>(S, tr, tq, sc, nullptr, stride, cnt, s_nodes, nl);
+                if (!fin) fin = trav_step<COUNT, ENV && NART_NODE_ROT_ENV>(S, tr, tq, sc, nullptr, stride, cnt, s_nodes, nl);
 #ifdef NART_WAVEPROF
                 if (COUNT && (tid8 >> 6) != 0u) { prof_shn += cnt.nodes - pn0; prof_sht += cnt.tris - pt0; }
 #endif

@@ -200,19 +200,18 @@ NHD inline uint32_t node_slot(uint32_t i) {
 #endif
 }
 NHD inline size_t node_lds_bytes(uint32_t n) { return (size_t)16 * (n ? node_slot(n - 1u) + 4u : 0u); }
-// LDS quarter of 16-B part k of BVH node i (stage_nodes, kernels.h)
+// LDS quarter of 16-B part k of BVH node i (stage_nodes, kernels.h).  ROT: rotate by (i >> 2) & 3
+// (the environment-light builds, whose larger BVHs gain from the bank spread; NART_NODE_SWZ=1: all)
+template <bool ROT = false>
 NHD inline uint32_t node_quarter(uint32_t i, uint32_t k) {
-#if NART_NODE_SWZ
-    return (k + (i >> 2)) & 3u;
-#else
+    if (ROT || NART_NODE_SWZ) return (k + (i >> 2)) & 3u;
     return k;
-#endif
 }
 #ifndef NART_TRI_PF
 #define NART_TRI_PF 2  // triangle records loaded per group in the leaf loop (0: one at a time)
 #endif
 #define NART_TRI_PAD 3  // padding records after tri_perm (a group of up to 4 may read past a leaf)
-template <bool COUNT>
+template <bool COUNT, bool ROT = false>
 ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, int stride, TraceCounters& cnt,
                   const float4* lnodes, int nl) {
     // (a wave-uniform node loop -- ballot per iteration, stopping once at most 0/2/4/8 lanes still
@@ -228,7 +227,7 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
             typedef float v4f __attribute__((ext_vector_type(4)));
             typedef const __attribute__((address_space(3))) v4f lds_v4f;
             lds_v4f* np = (lds_v4f*)lnodes + node_slot((uint32_t)t.code);
-            const uint32_t r = node_quarter((uint32_t)t.code, 0u);
+            const uint32_t r = node_quarter<ROT>((uint32_t)t.code, 0u);
             const v4f qa = np[r], qb = np[(r + 1u) & 3u], qc = np[(r + 2u) & 3u], qk = np[(r + 3u) & 3u];
             a = make_float4(qa.x, qa.y, qa.z, qa.w);
             b = make_float4(qb.x, qb.y, qb.z, qb.w);
@@ -247,7 +246,7 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
             typedef float v4f __attribute__((ext_vector_type(4)));
             typedef const __attribute__((address_space(3))) v4f lds_v4f;
             lds_v4f* np = (lds_v4f*)lnodes + node_slot((uint32_t)t.code);
-            const uint32_t r = node_quarter((uint32_t)t.code, 0u);
+            const uint32_t r = node_quarter<ROT>((uint32_t)t.code, 0u);
             const v4f qa = np[r], qb = np[(r + 1u) & 3u], qc = np[(r + 2u) & 3u], qk = np[(r + 3u) & 3u];
             a = make_float4(qa.x, qa.y, qa.z, qa.w);
             b = make_float4(qb.x, qb.y, qb.z, qb.w);
@@ -255,7 +254,7 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
             k = make_int4(__float_as_int(qk.x), __float_as_int(qk.y), __float_as_int(qk.z), __float_as_int(qk.w));
 #else
             const float4* np = lnodes + node_slot((uint32_t)t.code);
-            const uint32_t r = node_quarter((uint32_t)t.code, 0u);
+            const uint32_t r = node_quarter<ROT>((uint32_t)t.code, 0u);
             a = np[r];
             b = np[(r + 1u) & 3u];
             c = np[(r + 2u) & 3u];
