@@ -1128,6 +1128,9 @@ NHD size_t rq_lds_bytes(uint32_t stack_depth, uint32_t block) {
 #ifndef NART_RQ_BLOCK
 #define NART_RQ_BLOCK 512
 #endif
+#ifndef NART_ONE_LIGHT_ENV
+#define NART_ONE_LIGHT_ENV 1  // the environment-light builds' single-light EstimateDirect path
+#endif
 #ifndef NART_NODE_ROT_ENV
 #define NART_NODE_ROT_ENV 1  // the environment-light builds rotate the LDS node quarters (path.h)
 #endif
@@ -1655,7 +1658,12 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
                 if (bounce == 0) alpha = 1.f;
                 const f3 wo = to_local(bsdf, neg(cur.d));
                 // ---- EstimateDirect (pathintegrator.cpp:38-121)
-                const DLight& Lg = cst(S.lights)[f2u8(gmin(draw(), ND_ONE_MINUS_EPS) * nL)];
+                const uint32_t lsel = f2u8(gmin(draw(), ND_ONE_MINUS_EPS) * nL);
+                const DLight& Lg = cst(S.lights)[lsel];
+                // One light (every BASELINE scene): the pick is 0 on every lane, so the
+                // environment-light build reads that light through a wave-uniform index (scalar
+                // loads of the light and its sampling tables); the other builds keep one path.
+                const bool one_light = ENV && NART_ONE_LIGHT_ENV && S.num_lights == 1u;
                 float sPdf = 0.f, lPdf = 0.f;
                 float sx = draw();
                 float sy = draw();
@@ -1668,7 +1676,8 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
                     float flip = wi.z > 0.f ? 1.f : -1.f;
                     f3 wW = to_world(bsdf, wi);
                     float lt = __builtin_inff();
-                    f3 Li = light_li<ENV>(S, Lg, is.p, wW, &lPdf, lt);
+                    f3 Li = one_light ? light_li<ENV>(S, uniform_light(S, 0u), is.p, wW, &lPdf, lt)
+                                      : light_li<ENV>(S, Lg, is.p, wW, &lPdf, lt);
                     float weight = 1.f;
                     bool add1 = true;
                     if (!(dflags & F_SPECULAR)) {
@@ -1687,7 +1696,8 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
                 float ly = draw();
                 f3 wiW;
                 float lt2 = __builtin_inff();
-                f3 Li2 = light_sample_li<ENV>(S, Lg, is.p, wiW, F2(lx, ly), lPdf, lt2);
+                f3 Li2 = one_light ? light_sample_li<ENV>(S, uniform_light(S, 0u), is.p, wiW, F2(lx, ly), lPdf, lt2)
+                                   : light_sample_li<ENV>(S, Lg, is.p, wiW, F2(lx, ly), lPdf, lt2);
                 f3 wi2 = to_local(bsdf, wiW);
                 if (lPdf > 0.f) {
                     float sp2;
