@@ -1128,8 +1128,8 @@ NHD size_t rq_lds_bytes(uint32_t stack_depth, uint32_t block) {
 #ifndef NART_RQ_BLOCK
 #define NART_RQ_BLOCK 512
 #endif
-#ifndef NART_ONE_LIGHT_ENV
-#define NART_ONE_LIGHT_ENV 1  // the environment-light builds' single-light EstimateDirect path
+#ifndef NART_ONE_LIGHT
+#define NART_ONE_LIGHT 1  // the single-light EstimateDirect path (k_render_rq)
 #endif
 #ifndef NART_NODE_ROT_ENV
 #define NART_NODE_ROT_ENV 1  // the environment-light builds rotate the LDS node quarters (path.h)
@@ -1660,10 +1660,11 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
                 // ---- EstimateDirect (pathintegrator.cpp:38-121)
                 const uint32_t lsel = f2u8(gmin(draw(), ND_ONE_MINUS_EPS) * nL);
                 const DLight& Lg = cst(S.lights)[lsel];
-                // One light (every BASELINE scene): the pick is 0 on every lane, so the
-                // environment-light build reads that light through a wave-uniform index (scalar
-                // loads of the light and its sampling tables); the other builds keep one path.
-                const bool one_light = ENV && NART_ONE_LIGHT_ENV && S.num_lights == 1u;
+                // One light (every BASELINE scene): the pick is 0 on every lane, so the light is
+                // read through a wave-uniform index (scalar loads of the light record and, for an
+                // environment light, its sampling tables): C3 / C2 frames -1.3 %, C4 -0.9 %
+                // (profiles/r05am_one_light_all.log, r05al_c4_one_light_ab.log)
+                const bool one_light = NART_ONE_LIGHT && S.num_lights == 1u;
                 float sPdf = 0.f, lPdf = 0.f;
                 float sx = draw();
                 float sy = draw();
