@@ -1005,7 +1005,12 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
 // stages).  Light loop bound (pathintegrator.cpp:167-182) and octree answer as in k_render_rq;
 // hit[sample] = closest triangle or NO_HIT.
 template <bool COUNT, bool ENV>
-__global__ __launch_bounds__(256) void k_primary(DScene S, RenderArgs A, uint32_t* hit) {
+#ifndef NART_PRIMARY_WAVES
+// minimum waves per SIMD requested for k_primary: 4 (36 VGPRs spilled, latency hidden by the fourth
+// wave) vs the allocator's 3: C3 23.05 -> 21.1 ms, C4 1080p/32 3.31 -> 3.21 ms (profiles/r05ao_primary_waves_ab.txt)
+#define NART_PRIMARY_WAVES 4
+#endif
+__global__ __launch_bounds__(256, NART_PRIMARY_WAVES) void k_primary(DScene S, RenderArgs A, uint32_t* hit) {
     extern __shared__ __attribute__((aligned(16))) int s_dyn[];
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     if (slot >= A.n_slots) return;
