@@ -59,6 +59,7 @@ typedef struct nart_render_stats {
 #define NART_SCHED_PRIMARY     0x80u /* camera rays traced first (k_primary)                       */
 #define NART_SCHED_SPLAT_ROWS  0x100u /* skewed-time splat, W lanes per tile column (k_splat_rows)  */
 #define NART_SCHED_HALF_WAVES  0x200u /* costliest pixels on one wave per SIMD, raised priority     */
+#define NART_SCHED_SPECIALIZED 0x400u /* a scene-specialised path-kernel build ran (nart_hip_set_specialize) */
 
 /* Upload the scene, build the device BVH.  device_id: HIP ordinal. */
 int nart_hip_create(const nart_scene_blob* scene, int device_id, nart_ctx** out);
@@ -179,6 +180,27 @@ int nart_hip_context_bvh(const nart_ctx* ctx, nart_bvh_info* out, double* build_
    1 (the wavefront variant, 2x slower) and 2 (variant 3 with a traversal quorum) were retired:
    NART_E_UNSUPPORTED. */
 int nart_hip_set_variant(nart_ctx* ctx, int variant);
+
+/* Scene-specialised path kernels (no reference counterpart; all builds render the same image).
+   The context derives a feature mask from the scene (material kinds, light kinds, textured
+   patterns, normal maps: NART_FT_* bits, device/path.h FT_*) and runs the ray-queue kernel built
+   for the first mask that covers it -- glassSphere's, the Cornell box's, C4's -- so that code for
+   kinds the scene lacks is not compiled into the kernel.  enable = 0 forces the generic build
+   (default 1).  nart_hip_scene_features reports the scene's mask and the mask of the build the
+   last render launched (0x3FF = generic). */
+int nart_hip_set_specialize(nart_ctx* ctx, int enable);
+int nart_hip_scene_features(const nart_ctx* ctx, uint32_t* features, uint32_t* build);
+#define NART_FT_LAMBERT 0x1u
+#define NART_FT_SPECULAR 0x2u
+#define NART_FT_GLASS 0x4u
+#define NART_FT_GLOSSY 0x8u
+#define NART_FT_PLASTIC 0x10u
+#define NART_FT_DISK 0x20u
+#define NART_FT_RING 0x40u
+#define NART_FT_ENVIRONMENT 0x80u
+#define NART_FT_TEXTURE 0x100u
+#define NART_FT_NORMAL_MAP 0x200u
+#define NART_FT_ALL 0x3FFu
 
 /* Splat kernel (all bit-identical): -1 = automatic (the default: 4 when the launch fills >= 1
    wave per SIMD, else 5), 4 = skewed-time tile columns over the pixel-major sample layout (each

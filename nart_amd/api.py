@@ -18,6 +18,7 @@ LIB_DIR = os.path.join(_HERE, "lib")
 NART_OK = 0
 ERRORS = {-1: "NART_E_INVALID", -2: "NART_E_IO", -3: "NART_E_HIP", -4: "NART_E_OOM", -5: "NART_E_RCCL",
           -6: "NART_E_UNSUPPORTED"}
+NART_E_UNSUPPORTED = -6
 
 PIXEL_FLOATS = 5  # struct Pixel { vec4 contribution; float filterWeightSum; } (render.h:18-21)
 
@@ -61,7 +62,12 @@ class BvhInfo(ctypes.Structure):
 # nart_render_stats.schedule bits (include/nart_hip.h NART_SCHED_*)
 SCHED = {"probe_queue": 0x1, "priority": 0x2, "spec_pairs": 0x4, "wave_groups": 0x8, "vol_queue": 0x10,
          "vol_sparse": 0x20, "splat_skew": 0x40, "primary": 0x80, "splat_rows": 0x100,
-         "half_waves": 0x200}
+         "half_waves": 0x200, "specialized": 0x400}
+
+# scene feature bits (include/nart_hip.h NART_FT_*; nart_hip_scene_features)
+FEATURES = {"lambert": 0x1, "specular": 0x2, "glass": 0x4, "glossy": 0x8, "plastic": 0x10, "disk": 0x20,
+            "ring": 0x40, "environment": 0x80, "texture": 0x100, "normal_map": 0x200}
+FT_ALL = 0x3FF
 
 
 class RenderStats(ctypes.Structure):
@@ -131,6 +137,8 @@ _HIP_SIGS = {
     "nart_hip_eval_sincos": (ctypes.c_int, [_P, _P, ctypes.c_uint32, _P, _P]),
     "nart_hip_set_variant": (ctypes.c_int, [_P, ctypes.c_int]),
     "nart_hip_set_splat_mode": (ctypes.c_int, [_P, ctypes.c_int]),
+    "nart_hip_set_specialize": (ctypes.c_int, [_P, ctypes.c_int]),
+    "nart_hip_scene_features": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
     "nart_hip_splat_thresholds": (ctypes.c_int, [ctypes.c_float, _P]),
     "nart_hip_env_search": (ctypes.c_int, [_P, ctypes.c_uint32, _P, ctypes.c_uint32, _P, _P]),
     "nart_hip_splat_lut": (ctypes.c_int, [ctypes.c_float, _P, ctypes.POINTER(ctypes.c_uint32),
@@ -169,6 +177,15 @@ def scene_lib():
     return _load("libnart_scene.so", _SCENE_SIGS)
 
 
+def _missing_entry(fn, path):
+    """Stand-in for an entry point an alternative build (NART_HIP_LIB) lacks: calling it raises
+    a NartError naming the symbol and the build instead of an AttributeError or a call through an
+    untyped pointer."""
+    def call(*args):
+        raise NartError(NART_E_UNSUPPORTED, "%s is not exported by the build %s" % (fn, path))
+    return call
+
+
 def hip_lib():
     # NART_HIP_LIB: an alternative build of the same ABI (A/B experiments, tools/ab.sh)
     alt = os.environ.get("NART_HIP_LIB")
@@ -179,6 +196,7 @@ def hip_lib():
             for fn, (res, args) in _HIP_SIGS.items():
                 f = getattr(lib, fn, None)  # an older build may lack newer entry points
                 if f is None:
+                    setattr(lib, fn, _missing_entry(fn, alt))
                     continue
                 f.restype = res
                 f.argtypes = args
@@ -365,6 +383,18 @@ class HipRenderer:
         splat, 3 = four tile pixels per lane, 1-0 = one pixel per lane (include/nart_hip.h);
         identical results."""
         self._check(self._lib.nart_hip_set_splat_mode(self._ctx, int(mode)))
+
+    def set_specialize(self, on):
+        """Scene-specialised path kernels (default on) or the generic build (off); identical
+        results (nart_hip_set_specialize)."""
+        self._check(self._lib.nart_hip_set_specialize(self._ctx, 1 if on else 0))
+
+    def scene_features(self):
+        """(the scene's feature mask, the mask of the path-kernel build the last render launched;
+        FT_ALL = generic), NART_FT_* bits (nart_hip_scene_features)."""
+        f, b = ctypes.c_uint32(), ctypes.c_uint32()
+        self._check(self._lib.nart_hip_scene_features(self._ctx, ctypes.byref(f), ctypes.byref(b)))
+        return f.value, b.value
 
     def _check(self, rc):
         if rc != NART_OK:

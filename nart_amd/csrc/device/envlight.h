@@ -18,7 +18,7 @@ ND float env_ptn_pdf(const DScene& S, const DLight& L, f2 st) {
 // ENV = false compiles the environment branch out (scenes without one): it costs registers.
 // theta_in: acosf(wi.z) already formed by the caller (k_render_volume_sm shares that evaluation
 // with its scattering phase), or NAN to form it here
-template <bool ENV = true>
+template <bool ENV = true, uint32_t FM = FT_ALL>
 ND f3 light_li(const DScene& S, const DLight& L, f3 p, f3 wi, float* pdf, float& tMax,
                float theta_in = __builtin_nanf("")) {
     if (ENV && L.type == NART_LIGHT_ENVIRONMENT) {
@@ -32,13 +32,13 @@ ND f3 light_li(const DScene& S, const DLight& L, f3 p, f3 wi, float* pdf, float&
             *pdf *= ND_ONE_OVER_PI * 0.25f / gabs(glibc_sinf(theta));
         }
         tMax = ENV_TMAX;
-        return muls(ptn_value(S, L.Le, est), L.intensity);
+        return muls(ptn_value<FM>(S, L.Le, est), L.intensity);
     }
     f2 st = F2(0.f, 0.f);
-    float lp = area_pdf(L, p, wi, st, tMax);
+    float lp = area_pdf<FM>(L, p, wi, st, tMax);
     if (lp > 0.f) {
         if (pdf) *pdf = lp;
-        return muls(ptn_value(S, L.Le, st), L.intensity);
+        return muls(ptn_value<FM>(S, L.Le, st), L.intensity);
     }
     return F3(0.f, 0.f, 0.f);
 }
@@ -52,24 +52,24 @@ ND const DLight& uniform_light(const DScene& S, uint32_t j) { return cst(S.light
 // ray the loop needs just the bound tMax (and whether it was lowered), which this sets exactly as
 // light_li does -- without the radiance: for the environment light the acosf / atan2f and the
 // texture fetch, a dependent global load.
-template <bool ENV = true>
+template <bool ENV = true, uint32_t FM = FT_ALL>
 ND void light_bound(const DLight& L, f3 p, f3 wi, float& tMax) {
     if (ENV && L.type == NART_LIGHT_ENVIRONMENT) {
         tMax = ENV_TMAX;
         return;
     }
     f2 st = F2(0.f, 0.f);
-    (void)area_pdf(L, p, wi, st, tMax);
+    (void)area_pdf<FM>(L, p, wi, st, tMax);
 }
 
 // Light::Sample_Li (disklight.cpp:25-60, ringlight.cpp:26-64)
-template <bool ENV = true>
+template <bool ENV = true, uint32_t FM = FT_ALL>
 ND f3 light_sample_li(const DScene& S, const DLight& L, f3 p, f3& wi, f2 sample, float& pdf, float& tMax) {
     if (ENV && L.type == NART_LIGHT_ENVIRONMENT) {
         // Pattern::Sample (constantpattern.cpp:3-14, texturepattern.cpp:130-158)
         f2 ps = sample;
         f3 Lv;
-        if (L.Le.type == NART_PTN_CONSTANT) {
+        if (!(FM & FT_TEX) || L.Le.type == NART_PTN_CONSTANT) {
             pdf = 1.f;
             Lv = F3(L.Le.v[0], L.Le.v[1], L.Le.v[2]);
         } else {
@@ -92,7 +92,7 @@ ND f3 light_sample_li(const DScene& S, const DLight& L, f3 p, f3& wi, f2 sample,
         return Lv;
     }
     f4 ds;
-    if (L.type == NART_LIGHT_RING) {
+    if ((FM & FT_RING) && L.type == NART_LIGHT_RING) {
         f2 r = uniform_sample_ring(sample, pdf, L.inner_ratio);
         ds = F4(r.x * L.radius, r.y * L.radius, 0.f, 1.f);
     } else {
@@ -107,7 +107,7 @@ ND f3 light_sample_li(const DScene& S, const DLight& L, f3 p, f3& wi, f2 sample,
     wi = sub(xyz(ds), p);
     float dist = sqrtf(wi.x * wi.x + wi.y * wi.y + wi.z * wi.z);
     wi = normalize(wi);
-    if (L.type == NART_LIGHT_RING) pdf /= (ND_PI * L.radius * L.radius);
+    if ((FM & FT_RING) && L.type == NART_LIGHT_RING) pdf /= (ND_PI * L.radius * L.radius);
     else pdf = L.pdf_area;
     float wiDotN = dot(neg(wi), n);
     if (wiDotN <= 0.f) {
@@ -116,7 +116,7 @@ ND f3 light_sample_li(const DScene& S, const DLight& L, f3 p, f3& wi, f2 sample,
     }
     pdf = pdf * ((dist * dist) / wiDotN);
     tMax = dist;
-    return muls(ptn_value(S, L.Le, st), L.intensity);
+    return muls(ptn_value<FM>(S, L.Le, st), L.intensity);
 }
 
 }  // namespace nd

@@ -1004,7 +1004,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
 // so their rays run nearly the same traversal (the path kernel's lanes are at unrelated path
 // stages).  Light loop bound (pathintegrator.cpp:167-182) and octree answer as in k_render_rq;
 // hit[sample] = closest triangle or NO_HIT.
-template <bool COUNT, bool ENV>
+template <bool COUNT, bool ENV, uint32_t FM = FT_ALL>
 #ifndef NART_PRIMARY_WAVES
 // minimum waves per SIMD requested for k_primary: 4 (36 VGPRs spilled, latency hidden by the fourth
 // wave) vs the allocator's 3: C3 23.05 -> 21.1 ms, C4 1080p/32 3.31 -> 3.21 ms (profiles/r05ao_primary_waves_ab.txt)
@@ -1024,7 +1024,7 @@ __global__ __launch_bounds__(256, NART_PRIMARY_WAVES) void k_primary(DScene S, R
         float lightTMax = __builtin_inff();
         for (uint32_t j = 0; j < S.num_lights; ++j) {
             float lt = __builtin_inff();
-            light_bound<ENV>(uniform_light(S, j), ray.o, ray.d, lt);  // only the bound: no radiance
+            light_bound<ENV, FM>(uniform_light(S, j), ray.o, ray.d, lt);  // only the bound: no radiance
             if (lt < lightTMax) lightTMax = lt;
         }
         float bt;
@@ -1142,7 +1142,7 @@ NHD size_t rq_lds_bytes(uint32_t stack_depth, uint32_t block) {
 // The counter pass (COUNT: untimed, its counts are per ray and do not depend on the schedule) runs
 // 256-lane blocks at one wave per SIMD, so its counters do not push the kernel past 256 VGPRs.
 #define RQ_BLOCK_OF(COUNT) ((COUNT) ? 256 : NART_RQ_BLOCK)
-template <bool EXT, bool COUNT, bool ENV>
+template <bool EXT, bool COUNT, bool ENV, uint32_t FM = FT_ALL>
 __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) void k_render_rq(DScene S, RenderArgs A) {
     extern __shared__ __attribute__((aligned(16))) int s_dyn[];
     const int tid = threadIdx.x;
@@ -1288,7 +1288,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
         lightHit = false;
         for (uint32_t j = 0; j < S.num_lights; ++j) {
             float lt = __builtin_inff();
-            light_bound<ENV>(uniform_light(S, j), o, d, lt);
+            light_bound<ENV, FM>(uniform_light(S, j), o, d, lt);
             if (lt < lightTMax) {
                 lightTMax = lt;
                 lightHit = true;
@@ -1300,7 +1300,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
     };
     auto light_le = [&](f3 o, f3 d) {
         float lt = __builtin_inff();
-        return light_li<ENV>(S, cst(S.lights)[lwin], o, d, nullptr, lt);
+        return light_li<ENV, FM>(S, cst(S.lights)[lwin], o, d, nullptr, lt);
     };
     auto draw = [&]() {
         ++nd;
@@ -1655,7 +1655,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
             Isect is;
             fill_isect(S, cur, hitg, is);
             BSDF bsdf;
-            create_bsdf(S, is, alphaTweak, bsdf);
+            create_bsdf<FM>(S, is, alphaTweak, bsdf);
             use1 = use2 = false;
             bool cont;
             f3 no, nd;
@@ -1676,14 +1676,14 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
                 float bsmp = draw();
                 uint32_t dflags = 0;
                 f3 wi;
-                f3 f = bsdf_sample_f<ENV>(bsdf, wo, wi, bsmp, F2(sx, sy), sPdf, dflags, true, eta_outer, nullptr,
+                f3 f = bsdf_sample_f<ENV, FM>(bsdf, wo, wi, bsmp, F2(sx, sy), sPdf, dflags, true, eta_outer, nullptr,
                                      nullptr);
                 if (sPdf > 0.f) {
                     float flip = wi.z > 0.f ? 1.f : -1.f;
                     f3 wW = to_world(bsdf, wi);
                     float lt = __builtin_inff();
-                    f3 Li = one_light ? light_li<ENV>(S, uniform_light(S, 0u), is.p, wW, &lPdf, lt)
-                                      : light_li<ENV>(S, Lg, is.p, wW, &lPdf, lt);
+                    f3 Li = one_light ? light_li<ENV, FM>(S, uniform_light(S, 0u), is.p, wW, &lPdf, lt)
+                                      : light_li<ENV, FM>(S, Lg, is.p, wW, &lPdf, lt);
                     float weight = 1.f;
                     bool add1 = true;
                     if (!(dflags & F_SPECULAR)) {
@@ -1702,12 +1702,12 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
                 float ly = draw();
                 f3 wiW;
                 float lt2 = __builtin_inff();
-                f3 Li2 = one_light ? light_sample_li<ENV>(S, uniform_light(S, 0u), is.p, wiW, F2(lx, ly), lPdf, lt2)
-                                   : light_sample_li<ENV>(S, Lg, is.p, wiW, F2(lx, ly), lPdf, lt2);
+                f3 Li2 = one_light ? light_sample_li<ENV, FM>(S, uniform_light(S, 0u), is.p, wiW, F2(lx, ly), lPdf, lt2)
+                                   : light_sample_li<ENV, FM>(S, Lg, is.p, wiW, F2(lx, ly), lPdf, lt2);
                 f3 wi2 = to_local(bsdf, wiW);
                 if (lPdf > 0.f) {
                     float sp2;
-                    const f3 fv = bsdf_f_pdf(bsdf, wo, wi2, true, eta_outer, sp2);
+                    const f3 fv = bsdf_f_pdf<FM>(bsdf, wo, wi2, true, eta_outer, sp2);
                     if (sp2 > 0.f) {
                         float weight = (lPdf * lPdf) / (sp2 * sp2 + lPdf * lPdf);
                         c2 = divs(muls(muls(mul(fv, Li2), gabs(wi2.z)), weight), lPdf);
@@ -1726,7 +1726,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
                 float bs2 = draw();
                 float cpdf = 0.f, alpha_i = 0.f;
                 f3 wic;
-                f3 fc = bsdf_sample_f<ENV>(bsdf, wo, wic, bs2, F2(a, b), cpdf, flags, false, eta_outer, &alpha_i,
+                f3 fc = bsdf_sample_f<ENV, FM>(bsdf, wo, wic, bs2, F2(a, b), cpdf, flags, false, eta_outer, &alpha_i,
                                       &eta_sampled);
                 if (cpdf <= 0.f) {
                     cont = false;
@@ -1744,7 +1744,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
                 nd = cur.d;
                 flags = F_TRANSMISSIVE;
                 float bs2 = draw();
-                eta_sampled = bsdf_sample_eta(bsdf, bs2);
+                eta_sampled = bsdf_sample_eta<FM>(bsdf, bs2);
                 cont = true;
                 have_ed = false;
             }

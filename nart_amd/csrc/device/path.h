@@ -13,6 +13,30 @@ namespace nd {
 
 enum { F_SPECULAR = 1, F_GLOSSY = 2, F_DIFFUSE = 4, F_TRANSMISSIVE = 8 };
 #define SHADOW_BIAS 0.001f
+
+// Scene feature mask (template parameter FM of the shading functions and k_render_rq): the
+// material, light and pattern kinds a scene holds (scene_features, render.hip).  A kernel built
+// for a mask compiles only those kinds' code -- no plastic lobes, ring lights, texture fetches or
+// normal-map frames in glassSphere's build -- and serves every scene whose mask it covers; FT_ALL
+// is the generic build.  Each kind's operations are unchanged, so every build renders the same bits.
+enum : uint32_t {
+    FT_LAMBERT = 1u << 0,   // diffusematerial.cpp
+    FT_SPECMAT = 1u << 1,   // specularmaterial.cpp
+    FT_GLASS = 1u << 2,     // glassmaterial.cpp
+    FT_GLOSSY = 1u << 3,    // glossydielectricmaterial.cpp
+    FT_PLASTIC = 1u << 4,   // plasticmaterial.cpp (the only two-lobe BSDF)
+    FT_DISK = 1u << 5,      // disklight.cpp
+    FT_RING = 1u << 6,      // ringlight.cpp
+    FT_ENV = 1u << 7,       // environmentlight.cpp
+    FT_TEX = 1u << 8,       // any TexturePattern (materials or light Le)
+    FT_NMAP = 1u << 9,      // any material with a normal map
+    FT_ALL = (1u << 10) - 1u
+};
+// BxDF kinds a mask can create (the roughening factor moves a material between its two kinds)
+NHD constexpr bool ft_lambert(uint32_t FM) { return (FM & (FT_LAMBERT | FT_PLASTIC)) != 0u; }
+NHD constexpr bool ft_ts(uint32_t FM) { return (FM & (FT_SPECMAT | FT_GLOSSY | FT_PLASTIC)) != 0u; }
+NHD constexpr bool ft_spec(uint32_t FM) { return ft_ts(FM); }
+NHD constexpr bool ft_diel(uint32_t FM) { return (FM & FT_GLASS) != 0u; }
 #define NO_HIT 0xFFFFFFFFu
 
 // ---------------------------------------------------------------- Ray (geometry.cpp:3-15)
@@ -646,8 +670,9 @@ ND f3 tex_fetch(const DScene& S, int tex, float su, float sv, int rough) {  // t
     if (rough) { rr *= rr; gg *= gg; bb *= bb; }
     return F3(rr, gg, bb);
 }
+template <uint32_t FM = FT_ALL>
 ND f3 ptn_value(const DScene& S, const DPattern& p, f2 st) {
-    if (p.type == NART_PTN_CONSTANT) return F3(p.v[0], p.v[1], p.v[2]);
+    if (!(FM & FT_TEX) || p.type == NART_PTN_CONSTANT) return F3(p.v[0], p.v[1], p.v[2]);
     return tex_fetch(S, p.tex, st.x, st.y, p.rough);
 }
 
@@ -787,13 +812,14 @@ ND float bxdf_eta(const BxDF& b) { return b.type == B_LAMBERT ? 0.f : b.eta; }
 // operations of those two functions, but the half vector, D and the Smith term of wo, which both
 // recompute, are evaluated once (every call site of the reference pairs them: BxDF::Sample_f ends
 // with Pdf and f, EstimateDirect's light strategy with Pdf and f).
+template <uint32_t FM = FT_ALL>
 ND f3 bxdf_f_pdf(const BxDF& b, f3 wo, f3 wi, bool uap, float eta_outer, float& pdf) {
     pdf = 0.f;
-    if (b.type == B_LAMBERT) {  // lambertbrdf.cpp:7-29
+    if (ft_lambert(FM) && b.type == B_LAMBERT) {  // lambertbrdf.cpp:7-29
         pdf = wi.z * ND_ONE_OVER_PI;
         return muls(b.rho, ND_ONE_OVER_PI);
     }
-    if (b.type == B_DIEL) {  // dielectricbrdf.cpp:31-80 (f), 187-225 (Pdf)
+    if (ft_diel(FM) && b.type == B_DIEL) {  // dielectricbrdf.cpp:31-80 (f), 187-225 (Pdf)
         // Reflection (wo.z * wi.z >= 0) and transmission evaluate the same chain -- half vector,
         // D, the Smith terms, Fresnel -- on different inputs: the reflection half vector is
         // normalize(wo + wi) = normalize(wo * 1 + wi * 1) (x * 1 is exact) and its Fresnel argument
@@ -836,7 +862,7 @@ ND f3 bxdf_f_pdf(const BxDF& b, f3 wo, f3 wi, bool uap, float eta_outer, float& 
         if (refl ? wo.z * wi.z == 0.f : Fr >= 1.f) return F3(0.f, 0.f, 0.f);
         return refl ? F3(qx, qy, qz) : mul(F3(qx, qx, qx), b.tau);
     }
-    if (b.type == B_TS) {  // torrancesparrowbrdf.cpp:32-51 (f), 109-124 (Pdf)
+    if (ft_ts(FM) && b.type == B_TS) {  // torrancesparrowbrdf.cpp:32-51 (f), 109-124 (Pdf)
         const float alpha = uap ? b.ap : b.a0;
         const f3 wh = normalize(add(wo, wi));
         const float d = D_ggx(alpha, wh);
@@ -855,15 +881,16 @@ ND f3 bxdf_f_pdf(const BxDF& b, f3 wo, f3 wi, bool uap, float eta_outer, float& 
     return F3(0.f, 0.f, 0.f);  // delta lobes: f == 0, Pdf == 0
 }
 
+template <uint32_t FM = FT_ALL>
 ND f3 bxdf_sample_f(const BxDF& b, f3 wo, f3& wi, float s1, f2 sample, float& pdf, uint32_t& flags, float* alpha_i,
                     bool uap, float eta_outer) {
-    if (b.type == B_LAMBERT) {  // lambertbrdf.cpp:13-22
+    if (ft_lambert(FM) && b.type == B_LAMBERT) {  // lambertbrdf.cpp:13-22
         if (alpha_i) *alpha_i = 1.f;
         flags = F_DIFFUSE;
         wi = cosine_sample_hemisphere(sample, pdf);
-        return bxdf_f(b, wo, wi, uap, eta_outer);
+        return muls(b.rho, ND_ONE_OVER_PI);  // bxdf_f of B_LAMBERT
     }
-    if (b.type == B_SPECULAR) {  // specularbrdf.cpp:14-36
+    if (ft_spec(FM) && b.type == B_SPECULAR) {  // specularbrdf.cpp:14-36
         if (alpha_i) *alpha_i = 0.f;
         flags = F_SPECULAR;
         wi = F3(-wo.x, -wo.y, wo.z);
@@ -871,7 +898,7 @@ ND f3 bxdf_sample_f(const BxDF& b, f3 wo, f3& wi, float s1, f2 sample, float& pd
         if (wi.z == 0.f) return F3(1.f, 1.f, 1.f);
         return divs(muls(b.rho, fresnel(eta_outer, b.eta, wi.z)), gabs(wi.z));
     }
-    if (b.type == B_SPECDIEL) {  // speculardielectricbrdf.cpp:15-89
+    if (ft_diel(FM) && b.type == B_SPECDIEL) {  // speculardielectricbrdf.cpp:15-89
         float eta_o = eta_outer, eta_i = b.eta;
         if (eta_o == eta_i) {
             wi = neg(wo);
@@ -908,7 +935,7 @@ ND f3 bxdf_sample_f(const BxDF& b, f3 wo, f3& wi, float s1, f2 sample, float& pd
         float q = ((eta_o / eta_i) * (eta_o / eta_i) * (1.f - Fr)) / gabs(wi.z);
         return mul(F3(q, q, q), b.tau);
     }
-    if (b.type == B_DIEL) {  // dielectricbrdf.cpp:82-183
+    if (ft_diel(FM) && b.type == B_DIEL) {  // dielectricbrdf.cpp:82-183
         float eta_o = eta_outer, eta_i = b.eta;
         if (eta_o == eta_i) {
             wi = neg(wo);
@@ -940,11 +967,12 @@ ND f3 bxdf_sample_f(const BxDF& b, f3 wo, f3& wi, float s1, f2 sample, float& pd
         if (tr) flags |= F_TRANSMISSIVE;
         wi = normalize(tr ? add(c, d) : reflect(wo, wh));
         float pp;
-        const f3 fr = bxdf_f_pdf(b, wo, wi, uap, eta_outer, pp);
+        const f3 fr = bxdf_f_pdf<FM>(b, wo, wi, uap, eta_outer, pp);
         pdf = pp * (rf ? Fr : (1.f - Fr));
         return fr;
     }
-    // B_TS: torrancesparrowbrdf.cpp:53-105
+    // B_TS: torrancesparrowbrdf.cpp:53-105 (a mask without it creates no other kind)
+    if (!ft_ts(FM)) return F3(0.f, 0.f, 0.f);
     float alpha = uap ? b.ap : b.a0;
     if (alpha_i) *alpha_i = alpha;
     flags = F_SPECULAR;
@@ -952,7 +980,7 @@ ND f3 bxdf_sample_f(const BxDF& b, f3 wo, f3& wi, float s1, f2 sample, float& pd
     if (alpha >= 1.0f) flags = F_DIFFUSE;
     f3 wh = sample_wh(wo, alpha, sample, false);
     wi = normalize(reflect(wo, wh));
-    return bxdf_f_pdf(b, wo, wi, uap, eta_outer, pdf);
+    return bxdf_f_pdf<FM>(b, wo, wi, uap, eta_outer, pdf);
 }
 
 // ---------------------------------------------------------------- BSDF (bxdf.cpp:24-115)
@@ -984,45 +1012,51 @@ ND float bsdf_pdf(const BSDF& s, f3 wo, f3 wi, bool uap, float eta_outer) {
     if (s.num > 1) pdf += bxdf_pdf(s.b[1], wo, wi, uap, eta_outer);
     return pdf / (float)s.num;
 }
+// number of lobes: two only for plastic (a mask without it knows the BSDF has one)
+template <uint32_t FM>
+ND uint32_t bsdf_num(const BSDF& s) { return (FM & FT_PLASTIC) ? s.num : 1u; }
 // bsdf_f and bsdf_pdf together (bxdf_f_pdf per lobe; the sums in the same order)
+template <uint32_t FM = FT_ALL>
 ND f3 bsdf_f_pdf(const BSDF& s, f3 wo, f3 wi, bool uap, float eta_outer, float& pdf) {
+    const uint32_t num = bsdf_num<FM>(s);
     float p0, p1 = 0.f;
     f3 f = F3(0.f, 0.f, 0.f);
-    f = add(f, bxdf_f_pdf(s.b[0], wo, wi, uap, eta_outer, p0));
+    f = add(f, bxdf_f_pdf<FM>(s.b[0], wo, wi, uap, eta_outer, p0));
     f3 f1 = F3(0.f, 0.f, 0.f);
-    if (s.num > 1) f1 = bxdf_f_pdf(s.b[1], wo, wi, uap, eta_outer, p1);
-    if (s.num > 1) f = add(f, f1);
+    if (num > 1) f1 = bxdf_f_pdf<FM>(s.b[1], wo, wi, uap, eta_outer, p1);
+    if (num > 1) f = add(f, f1);
     float p = 0.f;
     p += p0;
-    if (s.num > 1) p += p1;
-    pdf = p / (float)s.num;
+    if (num > 1) p += p1;
+    pdf = p / (float)num;
     return f;
 }
 // SHARE_TS: the environment-light builds of the path kernels (C4: 3,332 -> 3,259 ms); the others
 // keep one evaluation per role (C3 measured 316 -> 322 ms with sharing, a register-allocation
 // effect in the 256-VGPR kernel, which has no plastic lobes to share; profiles/r04y_share_ts_ab.log)
-template <bool SHARE_TS = true>
+template <bool SHARE_TS = true, uint32_t FM = FT_ALL>
 ND f3 bsdf_sample_f(const BSDF& s, f3 wo, f3& wi, float s1, f2 sample, float& pdf, uint32_t& flags, bool uap,
                     float eta_outer, float* alpha_i, float* eta_i) {
-    if (!SHARE_TS) {
-        uint32_t idx = f2u8(s1 * (float)s.num);
-        s1 = gfract(s1 * (float)s.num);
-        const BxDF& sel = s.b[idx ? 1 : 0];
-        f3 f = bxdf_sample_f(sel, wo, wi, s1, sample, pdf, flags, alpha_i, uap, eta_outer);
+    const uint32_t num = bsdf_num<FM>(s);
+    if (!SHARE_TS || !(FM & FT_PLASTIC)) {
+        uint32_t idx = f2u8(s1 * (float)num);
+        s1 = gfract(s1 * (float)num);
+        const BxDF& sel = s.b[((FM & FT_PLASTIC) && idx) ? 1 : 0];
+        f3 f = bxdf_sample_f<FM>(sel, wo, wi, s1, sample, pdf, flags, alpha_i, uap, eta_outer);
         if (eta_i && (flags & F_TRANSMISSIVE)) *eta_i = bxdf_eta(sel);
         if (!(flags & F_SPECULAR)) {
-            if (s.num > 1) {
+            if (num > 1) {
                 const BxDF& o = s.b[idx ? 0 : 1];
                 if (!(o.flags & F_SPECULAR)) {
                     float bp;
-                    const f3 fo = bxdf_f_pdf(o, wo, wi, uap, eta_outer, bp);
+                    const f3 fo = bxdf_f_pdf<FM>(o, wo, wi, uap, eta_outer, bp);
                     if (bp > 0.f) {
                         pdf += bp;
                         f = add(f, fo);
                     }
                 }
             }
-            pdf /= (float)s.num;
+            pdf /= (float)num;
         }
         return f;
     }
@@ -1035,7 +1069,7 @@ ND f3 bsdf_sample_f(const BSDF& s, f3 wo, f3& wi, float s1, f2 sample, float& pd
     // (bxdf.cpp:87-106): a wave holding both kinds of lanes ran that evaluation twice.  Here the
     // B_TS sampling step only draws wi, and one bxdf_f_pdf serves both roles, with the lane's own
     // lobe and wi (the sums below take the same operands; + is commutative).
-    const bool ts_sel = sel.type == B_TS;
+    const bool ts_sel = ft_ts(FM) && sel.type == B_TS;
     f3 f = F3(0.f, 0.f, 0.f);
     if (ts_sel) {  // torrancesparrowbrdf.cpp:53-105 up to the direction
         float alpha = uap ? sel.ap : sel.a0;
@@ -1046,7 +1080,7 @@ ND f3 bsdf_sample_f(const BSDF& s, f3 wo, f3& wi, float s1, f2 sample, float& pd
         f3 wh = sample_wh(wo, alpha, sample, false);
         wi = normalize(reflect(wo, wh));
     } else {
-        f = bxdf_sample_f(sel, wo, wi, s1, sample, pdf, flags, alpha_i, uap, eta_outer);
+        f = bxdf_sample_f<FM>(sel, wo, wi, s1, sample, pdf, flags, alpha_i, uap, eta_outer);
     }
     if (eta_i && (flags & F_TRANSMISSIVE)) *eta_i = bxdf_eta(sel);
     // (o is read only for two-lobe BSDFs: s.num > 1 is tested first)
@@ -1054,7 +1088,7 @@ ND f3 bsdf_sample_f(const BSDF& s, f3 wo, f3& wi, float s1, f2 sample, float& pd
     const bool other_ts = other && !ts_sel && o.type == B_TS;
     float tp = 0.f;
     f3 tf = F3(0.f, 0.f, 0.f);
-    if (ts_sel || other_ts) tf = bxdf_f_pdf(ts_sel ? sel : o, wo, wi, uap, eta_outer, tp);
+    if (ts_sel || other_ts) tf = bxdf_f_pdf<FM>(ts_sel ? sel : o, wo, wi, uap, eta_outer, tp);
     if (ts_sel) {
         f = tf;
         pdf = tp;
@@ -1063,7 +1097,7 @@ ND f3 bsdf_sample_f(const BSDF& s, f3 wo, f3& wi, float s1, f2 sample, float& pd
         if (other) {
             float bp = tp;
             f3 fo = tf;
-            if (!other_ts) fo = bxdf_f_pdf(o, wo, wi, uap, eta_outer, bp);
+            if (!other_ts) fo = bxdf_f_pdf<FM>(o, wo, wi, uap, eta_outer, bp);
             if (bp > 0.f) {
                 pdf += bp;
                 f = add(f, fo);
@@ -1073,15 +1107,23 @@ ND f3 bsdf_sample_f(const BSDF& s, f3 wo, f3& wi, float s1, f2 sample, float& pd
     }
     return f;
 }
-ND float bsdf_sample_eta(const BSDF& s, float s1) { return bxdf_eta(s.b[f2u8(s1 * (float)s.num) ? 1 : 0]); }
+template <uint32_t FM = FT_ALL>
+ND float bsdf_sample_eta(const BSDF& s, float s1) {
+    return bxdf_eta(s.b[((FM & FT_PLASTIC) && f2u8(s1 * (float)s.num)) ? 1 : 0]);
+}
 
-// Material::CreateBSDF (src/materials/*.cpp)
+// Material::CreateBSDF (src/materials/*.cpp).  A material kind outside FM is never tested; the
+// last kind in the mask takes every remaining material (as the generic switch's default does).
+template <uint32_t FM = FT_ALL>
 ND void create_bsdf(const DScene& S, const Isect& is, float alphaTweak, BSDF& bs) {
     const DMaterial& m = cst(S.mats)[is.mat];
+    constexpr uint32_t MM = FM & (FT_LAMBERT | FT_SPECMAT | FT_GLASS | FT_GLOSSY | FT_PLASTIC);
+    constexpr uint32_t last = MM ? (1u << (31 - __builtin_clz(MM | 1u))) : FT_PLASTIC;
+    const int32_t t = m.type;
     bs.n = is.sn;
-    bs.num = m.type == NART_MAT_PLASTIC ? 2u : 1u;
-    if (m.has_normal) {
-        f3 n = ptn_value(S, m.normal, is.st);
+    bs.num = ((FM & FT_PLASTIC) && t == NART_MAT_PLASTIC) ? 2u : 1u;
+    if ((FM & FT_NMAP) && m.has_normal) {
+        f3 n = ptn_value<FM>(S, m.normal, is.st);
         n = muls(n, 2.f);
         n = sub(n, F3(1.f, 1.f, 1.f));
         build_coord_sys(bs, is, &n);
@@ -1093,57 +1135,47 @@ ND void create_bsdf(const DScene& S, const Isect& is, float alphaTweak, BSDF& bs
     b0.eta = 0.f;
     b0.a0 = 0.f;
     b0.ap = 0.f;
-    switch (m.type) {
-        case NART_MAT_LAMBERT:  // diffusematerial.cpp:6-27
-            b0.type = B_LAMBERT;
-            b0.flags = F_DIFFUSE;
-            b0.rho = ptn_value(S, m.rho_d, is.st);
-            break;
-        case NART_MAT_SPECULAR: {  // specularmaterial.cpp:9-43
-            float alpha = 0.f;
-            float ap = 1.f - ((1.f - alpha) * alphaTweak);
-            b0.rho = ptn_value(S, m.rho_s, is.st);
-            b0.eta = ptn_value(S, m.eta, is.st).x;
-            if (ap > 0.0001f) { b0.type = B_TS; b0.flags = F_GLOSSY; b0.a0 = gmax(0.0001f, alpha); b0.ap = ap; }
-            else { b0.type = B_SPECULAR; b0.flags = F_SPECULAR; }
-            break;
-        }
-        case NART_MAT_GLASS: {  // glassmaterial.cpp:11-47
-            float alpha = ptn_value(S, m.alpha, is.st).x;
-            float ap = 1.f - ((1.f - ptn_value(S, m.alpha, is.st).x) * alphaTweak);
-            b0.rho = ptn_value(S, m.rho_s, is.st);
-            b0.tau = ptn_value(S, m.tau, is.st);
-            b0.eta = ptn_value(S, m.eta, is.st).x;
-            if (ap > 0.0001f) { b0.type = B_DIEL; b0.flags = F_GLOSSY; b0.a0 = gmax(0.0001f, alpha); b0.ap = ap; }
-            else { b0.type = B_SPECDIEL; b0.flags = F_SPECULAR; }
-            break;
-        }
-        case NART_MAT_GLOSSY: {  // glossydielectricmaterial.cpp:12-47
-            float alpha = ptn_value(S, m.alpha, is.st).x;
-            float ap = 1.f - ((1.f - alpha) * alphaTweak);
-            b0.rho = ptn_value(S, m.rho_s, is.st);
-            b0.eta = ptn_value(S, m.eta, is.st).x;
-            if (ap > 0.0001f) { b0.type = B_TS; b0.flags = F_GLOSSY; b0.a0 = gmax(0.0001f, alpha); b0.ap = ap; }
-            else { b0.type = B_SPECULAR; b0.flags = F_SPECULAR; }
-            break;
-        }
-        default: {  // NART_MAT_PLASTIC: plasticmaterial.cpp:12-51
-            float alpha = ptn_value(S, m.alpha, is.st).x;
-            float ap = 1.f - ((1.f - alpha) * alphaTweak);
-            f3 rho_d = ptn_value(S, m.rho_d, is.st);
-            f3 rho_s = ptn_value(S, m.rho_s, is.st);
-            float eta = ptn_value(S, m.eta, is.st).x;
-            b0.type = B_LAMBERT;
-            b0.flags = F_DIFFUSE;
-            b0.rho = rho_d;
-            BxDF& b1 = bs.b[1];
-            b1.rho = rho_s;
-            b1.tau = F3(0.f, 0.f, 0.f);
-            b1.eta = eta;
-            if (ap > 0.001f) { b1.type = B_TS; b1.flags = F_GLOSSY; b1.a0 = gmax(0.0001f, alpha); b1.ap = ap; }
-            else { b1.type = B_SPECULAR; b1.flags = F_SPECULAR; b1.a0 = 0.f; b1.ap = 0.f; }
-            break;
-        }
+    if ((FM & FT_LAMBERT) && (last == FT_LAMBERT || t == NART_MAT_LAMBERT)) {  // diffusematerial.cpp:6-27
+        b0.type = B_LAMBERT;
+        b0.flags = F_DIFFUSE;
+        b0.rho = ptn_value<FM>(S, m.rho_d, is.st);
+    } else if ((FM & FT_SPECMAT) && (last == FT_SPECMAT || t == NART_MAT_SPECULAR)) {  // specularmaterial.cpp:9-43
+        float alpha = 0.f;
+        float ap = 1.f - ((1.f - alpha) * alphaTweak);
+        b0.rho = ptn_value<FM>(S, m.rho_s, is.st);
+        b0.eta = ptn_value<FM>(S, m.eta, is.st).x;
+        if (ap > 0.0001f) { b0.type = B_TS; b0.flags = F_GLOSSY; b0.a0 = gmax(0.0001f, alpha); b0.ap = ap; }
+        else { b0.type = B_SPECULAR; b0.flags = F_SPECULAR; }
+    } else if ((FM & FT_GLASS) && (last == FT_GLASS || t == NART_MAT_GLASS)) {  // glassmaterial.cpp:11-47
+        float alpha = ptn_value<FM>(S, m.alpha, is.st).x;
+        float ap = 1.f - ((1.f - ptn_value<FM>(S, m.alpha, is.st).x) * alphaTweak);
+        b0.rho = ptn_value<FM>(S, m.rho_s, is.st);
+        b0.tau = ptn_value<FM>(S, m.tau, is.st);
+        b0.eta = ptn_value<FM>(S, m.eta, is.st).x;
+        if (ap > 0.0001f) { b0.type = B_DIEL; b0.flags = F_GLOSSY; b0.a0 = gmax(0.0001f, alpha); b0.ap = ap; }
+        else { b0.type = B_SPECDIEL; b0.flags = F_SPECULAR; }
+    } else if ((FM & FT_GLOSSY) && (last == FT_GLOSSY || t == NART_MAT_GLOSSY)) {  // glossydielectricmaterial.cpp:12-47
+        float alpha = ptn_value<FM>(S, m.alpha, is.st).x;
+        float ap = 1.f - ((1.f - alpha) * alphaTweak);
+        b0.rho = ptn_value<FM>(S, m.rho_s, is.st);
+        b0.eta = ptn_value<FM>(S, m.eta, is.st).x;
+        if (ap > 0.0001f) { b0.type = B_TS; b0.flags = F_GLOSSY; b0.a0 = gmax(0.0001f, alpha); b0.ap = ap; }
+        else { b0.type = B_SPECULAR; b0.flags = F_SPECULAR; }
+    } else if (FM & FT_PLASTIC) {  // NART_MAT_PLASTIC: plasticmaterial.cpp:12-51
+        float alpha = ptn_value<FM>(S, m.alpha, is.st).x;
+        float ap = 1.f - ((1.f - alpha) * alphaTweak);
+        f3 rho_d = ptn_value<FM>(S, m.rho_d, is.st);
+        f3 rho_s = ptn_value<FM>(S, m.rho_s, is.st);
+        float eta = ptn_value<FM>(S, m.eta, is.st).x;
+        b0.type = B_LAMBERT;
+        b0.flags = F_DIFFUSE;
+        b0.rho = rho_d;
+        BxDF& b1 = bs.b[1];
+        b1.rho = rho_s;
+        b1.tau = F3(0.f, 0.f, 0.f);
+        b1.eta = eta;
+        if (ap > 0.001f) { b1.type = B_TS; b1.flags = F_GLOSSY; b1.a0 = gmax(0.0001f, alpha); b1.ap = ap; }
+        else { b1.type = B_SPECULAR; b1.flags = F_SPECULAR; b1.a0 = 0.f; b1.ap = 0.f; }
     }
 }
 
@@ -1202,6 +1234,7 @@ ND f2 env_sample(const DEnvDist& d, f2 s, float& pdf) {  // texturepattern.cpp:7
 }
 
 // Disk / ring Pdf (disklight.cpp:62-104, ringlight.cpp:66-112); sets st and tMax on a hit.
+template <uint32_t FM = FT_ALL>
 ND float area_pdf(const DLight& L, f3 p, f3 wi, f2& st, float& tMax) {
     f3 n = load3(L.n);
     if (dot(wi, n) >= 0.f) return 0.f;
@@ -1217,7 +1250,7 @@ ND float area_pdf(const DLight& L, f3 p, f3 wi, f2& st, float& tMax) {
     st = F2(u, 1.f - v);
     float dist = c2p.x * c2p.x + c2p.y * c2p.y + c2p.z * c2p.z;
     if (dist > L.r2) return 0.f;
-    if (L.type == NART_LIGHT_RING && dist < L.ri2) return 0.f;
+    if ((FM & FT_RING) && L.type == NART_LIGHT_RING && dist < L.ri2) return 0.f;
     float pdf = L.pdf_area;
     pdf = pdf * ((t * t) / dot(neg(wi), n));
     tMax = t;

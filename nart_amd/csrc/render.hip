@@ -33,6 +33,9 @@ struct nart_ctx {
     int splat_mode = -1;  // -1: automatic (render_buckets)
     bool counters = false;
     bool has_env = false;  // scene has an environment light (selects the k_render build)
+    uint32_t features = FT_ALL;  // scene feature mask (scene_features): selects the k_render_rq build
+    bool specialize = true;      // nart_hip_set_specialize: scene-specialised path kernels
+    uint32_t fm_used = FT_ALL;   // the feature mask of the last path-kernel build launched
     // scene buffers
     void* d_nodes = nullptr;
     void* d_tri_isect = nullptr;
@@ -130,6 +133,41 @@ int upload(nart_ctx* ctx, void*& dst, const T* src, size_t count) {
     HIPCHK(hipMalloc(&dst, bytes));
     if (count) HIPCHK(hipMemcpy(dst, src, sizeof(T) * count, hipMemcpyHostToDevice));
     return NART_OK;
+}
+
+// Feature mask of a scene (FT_*, path.h): every material kind, light kind, textured pattern and
+// normal map the scene's records hold.  A path kernel built for a mask covering it compiles only
+// that code; unknown kinds give FT_ALL (the generic build).
+uint32_t scene_features(const std::vector<DMaterial>& mats, const std::vector<DLight>& lights) {
+    uint32_t f = 0;
+    auto ptn = [&](const DPattern& p) {
+        if (p.type != NART_PTN_CONSTANT) f |= FT_TEX;
+    };
+    for (const DMaterial& m : mats) {
+        switch (m.type) {
+            case NART_MAT_LAMBERT: f |= FT_LAMBERT; break;
+            case NART_MAT_SPECULAR: f |= FT_SPECMAT; break;
+            case NART_MAT_GLASS: f |= FT_GLASS; break;
+            case NART_MAT_GLOSSY: f |= FT_GLOSSY; break;
+            case NART_MAT_PLASTIC: f |= FT_PLASTIC; break;
+            default: return FT_ALL;
+        }
+        for (const DPattern* p : {&m.rho_d, &m.rho_s, &m.tau, &m.eta, &m.alpha}) ptn(*p);
+        if (m.has_normal) {
+            f |= FT_NMAP;
+            ptn(m.normal);
+        }
+    }
+    for (const DLight& L : lights) {
+        switch (L.type) {
+            case NART_LIGHT_DISK: f |= FT_DISK; break;
+            case NART_LIGHT_RING: f |= FT_RING; break;
+            case NART_LIGHT_ENVIRONMENT: f |= FT_ENV; break;
+            default: return FT_ALL;
+        }
+        ptn(L.Le);
+    }
+    return f;
 }
 
 DPattern dpat(const nart_pattern& p) {
@@ -630,10 +668,10 @@ int sort_groups_by_cost(nart_ctx* ctx, uint32_t n, uint32_t* out, hipStream_t st
     return NART_OK;
 }
 
-template <bool EXT, bool COUNT, bool ENV>
+template <bool EXT, bool COUNT, bool ENV, uint32_t FM = FT_ALL>
 int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
     auto kern = k_render<EXT, COUNT, ENV>;
-    auto kern_rq = k_render_rq<EXT, COUNT, ENV>;
+    auto kern_rq = k_render_rq<EXT, COUNT, ENV, FM>;
     constexpr uint32_t RQB = RQ_BLOCK_OF(COUNT);  // ray-queue block (kernels.h)
     RenderArgs a = a_in;
     if (EXT) {
@@ -655,7 +693,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
     const uint64_t dbit = 1ull << (ctx->device & 63);
     if (!(attr.load() & dbit)) {
         for (const void* f : {(const void*)kern, (const void*)k_render<EXT, true, ENV>,
-                              (const void*)kern_rq, (const void*)k_primary<COUNT, ENV>})
+                              (const void*)kern_rq, (const void*)k_primary<COUNT, ENV, FM>})
             hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr.fetch_or(dbit);
     }
@@ -664,6 +702,8 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
     // 60 KiB of ray outboxes in LDS: a BVH deeper than 24 levels does not fit, and those scenes
     // run k_render (256-lane blocks, stack_depth * 2 KiB) instead -- same image.
     const bool rq = ctx->variant == 0 && rq_fits(ctx);
+    ctx->fm_used = rq ? FM : FT_ALL;
+    if (rq && FM != FT_ALL) ctx->sched |= NART_SCHED_SPECIALIZED;
     // camera rays first, coherently (k_primary); NART_PRIMARY=0 leaves them to the path kernel
     const bool primary = !std::getenv("NART_PRIMARY") || std::atoi(std::getenv("NART_PRIMARY")) != 0;
 
@@ -682,7 +722,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
         RenderArgs pa = a;
         const char* pp = std::getenv("NART_PRIMARY_PACKET");
         pa.packet = pp ? (uint32_t)(std::atoi(pp) != 0) : 1u;
-        hipLaunchKernelGGL((k_primary<COUNT, ENV>), dim3((a.n_slots + 255) / 256), dim3(256),
+        hipLaunchKernelGGL((k_primary<COUNT, ENV, FM>), dim3((a.n_slots + 255) / 256), dim3(256),
                            (size_t)ctx->stack_depth * 256 * 8, st, ctx->scene, pa, ctx->d_prim);
         HIPCHK(hipGetLastError());
         if (ctx->events) {
@@ -895,7 +935,24 @@ int launch_render_maxl(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     return c ? launch_render<true, true, ENV>(ctx, a, st) : launch_render<true, false, ENV>(ctx, a, st);
 }
 
+// Scene-specialised builds of the path kernels (k_render_rq, k_primary): glassSphere's (C3:
+// Lambert + glass, one kind of area light, constant patterns), the Cornell box's (C2: Lambert,
+// disk) and the textured environment-lit plastic of C4.  A render takes the first build whose mask
+// covers the scene's (ctx->features); others, the counter pass and renders with bounces > ILIST_REG
+// run the generic build.  Same operations per kind, so every build renders the same image
+// (tests/test_gpu_specialize.py compares them on every suite scene).
+constexpr uint32_t FM_DIFFUSE = FT_LAMBERT | FT_DISK;
+constexpr uint32_t FM_GLASS = FT_LAMBERT | FT_GLASS | FT_DISK;
+constexpr uint32_t FM_ENVTEX = FT_LAMBERT | FT_PLASTIC | FT_ENV | FT_TEX | FT_NMAP;
+
 int dispatch_megakernel(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
+    const uint32_t f = ctx->features;
+    auto covers = [f](uint32_t m) { return (f & ~m) == 0u; };
+    if (ctx->specialize && !ctx->counters && a.bounces <= ILIST_REG) {
+        if (!ctx->has_env && covers(FM_DIFFUSE)) return launch_render<false, false, false, FM_DIFFUSE>(ctx, a, st);
+        if (!ctx->has_env && covers(FM_GLASS)) return launch_render<false, false, false, FM_GLASS>(ctx, a, st);
+        if (ctx->has_env && covers(FM_ENVTEX)) return launch_render<false, false, true, FM_ENVTEX>(ctx, a, st);
+    }
     return ctx->has_env ? launch_render_maxl<true>(ctx, a, st) : launch_render_maxl<false>(ctx, a, st);
 }
 
@@ -1730,6 +1787,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     }
     if ((rc = upload(ctx, ctx->d_envs, envs.data(), envs.size()))) return bail(rc);
     if ((rc = upload(ctx, ctx->d_lights, lights.data(), lights.size()))) return bail(rc);
+    ctx->features = scene_features(mats, lights);
     std::vector<DTexture> texs(blob->num_textures);
     size_t pool = 0;
     for (uint32_t t = 0; t < blob->num_textures; ++t) {
@@ -1848,6 +1906,21 @@ int nart_hip_set_splat_mode(nart_ctx* ctx, int mode) {
                                              "tile columns, 3 four pixels per lane, 1-0 one pixel per lane; the "
                                              "LDS-staged and tile-column-sweep modes were retired, DESIGN.md)");
     ctx->splat_mode = mode;
+    return NART_OK;
+}
+
+int nart_hip_set_specialize(nart_ctx* ctx, int enable) {
+    if (!ctx) return NART_E_INVALID;
+    ctx->specialize = enable != 0;
+    for (nart_ctx* c : ctx->subs) c->specialize = ctx->specialize;
+    return NART_OK;
+}
+
+int nart_hip_scene_features(const nart_ctx* ctx, uint32_t* features, uint32_t* build) {
+    if (!ctx) return NART_E_INVALID;
+    const nart_ctx* c = ctx->subs.empty() ? ctx : ctx->subs[0];
+    if (features) *features = c->features;
+    if (build) *build = c->fm_used;
     return NART_OK;
 }
 

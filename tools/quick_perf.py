@@ -19,6 +19,7 @@ def main():
     ap.add_argument("-H", type=int, default=1080)
     ap.add_argument("-s", type=int, default=16)
     ap.add_argument("--counters", action="store_true")
+    ap.add_argument("--generic", action="store_true", help="the generic path-kernel build (no scene specialisation)")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--bounces", type=int, default=0, help="override the scene's bounce limit")
     ap.add_argument("--env", type=int, default=1024, help="c4: environment map width (height = width / 2)")
@@ -46,6 +47,8 @@ def main():
     if a.bounces:
         p.bounces = a.bounces
     r = nart_amd.HipRenderer(scene)
+    if a.generic:
+        r.set_specialize(False)
     for rep in range(a.reps):
         st = nart_amd.RenderStats()
         t = time.time()
@@ -55,6 +58,7 @@ def main():
         d["wall_s"] = dt
         d["msamples_per_s_kernel"] = d["samples"] / (d["kernel_ms"] * 1e3)
         d["msamples_per_s_wall"] = d["samples"] / dt / 1e6
+        d["features"], d["build"] = r.scene_features()
         print(json.dumps(d), flush=True)
     if a.counters:
         r.set_counters(True)
