@@ -60,6 +60,7 @@ typedef struct nart_render_stats {
 #define NART_SCHED_SPLAT_ROWS  0x100u /* skewed-time splat, W lanes per tile column (k_splat_rows)  */
 #define NART_SCHED_HALF_WAVES  0x200u /* costliest pixels on one wave per SIMD, raised priority     */
 #define NART_SCHED_SPECIALIZED 0x400u /* a scene-specialised path-kernel build ran (nart_hip_set_specialize) */
+#define NART_SCHED_LEAN        0x800u /* the lean three-waves-per-SIMD build of a throughput-bound launch */
 
 /* Upload the scene, build the device BVH.  device_id: HIP ordinal. */
 int nart_hip_create(const nart_scene_blob* scene, int device_id, nart_ctx** out);
@@ -185,10 +186,12 @@ int nart_hip_set_variant(nart_ctx* ctx, int variant);
    The context derives a feature mask from the scene (material kinds, light kinds, textured
    patterns, normal maps: NART_FT_* bits, device/path.h FT_*) and runs the ray-queue kernel built
    for the first mask that covers it -- glassSphere's, the Cornell box's, C4's -- so that code for
-   kinds the scene lacks is not compiled into the kernel.  enable = 0 forces the generic build
-   (default 1).  nart_hip_scene_features reports the scene's mask and the mask of the build the
-   last render launched (0x3FF = generic). */
-int nart_hip_set_specialize(nart_ctx* ctx, int enable);
+   kinds the scene lacks is not compiled into the kernel; throughput-bound launches (whole frames)
+   of scenes whose traversal stack fits take the lean build of that mask (no priority lanes or
+   speculative pairs, three waves per SIMD: NART_SCHED_LEAN).  mode 0 forces the generic build, 1
+   the specialised builds without the lean one, 2 (default) all of them.  nart_hip_scene_features
+   reports the scene's mask and the mask of the build the last render launched (0x3FF = generic). */
+int nart_hip_set_specialize(nart_ctx* ctx, int mode);
 int nart_hip_scene_features(const nart_ctx* ctx, uint32_t* features, uint32_t* build);
 #define NART_FT_LAMBERT 0x1u
 #define NART_FT_SPECULAR 0x2u

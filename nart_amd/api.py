@@ -62,7 +62,8 @@ class BvhInfo(ctypes.Structure):
 # nart_render_stats.schedule bits (include/nart_hip.h NART_SCHED_*)
 SCHED = {"probe_queue": 0x1, "priority": 0x2, "spec_pairs": 0x4, "wave_groups": 0x8, "vol_queue": 0x10,
          "vol_sparse": 0x20, "splat_skew": 0x40, "primary": 0x80, "splat_rows": 0x100,
-         "half_waves": 0x200, "specialized": 0x400}
+         "half_waves": 0x200, "specialized": 0x400,
+         "lean": 0x800}
 
 # scene feature bits (include/nart_hip.h NART_FT_*; nart_hip_scene_features)
 FEATURES = {"lambert": 0x1, "specular": 0x2, "glass": 0x4, "glossy": 0x8, "plastic": 0x10, "disk": 0x20,
@@ -384,10 +385,12 @@ class HipRenderer:
         identical results."""
         self._check(self._lib.nart_hip_set_splat_mode(self._ctx, int(mode)))
 
-    def set_specialize(self, on):
-        """Scene-specialised path kernels (default on) or the generic build (off); identical
-        results (nart_hip_set_specialize)."""
-        self._check(self._lib.nart_hip_set_specialize(self._ctx, 1 if on else 0))
+    def set_specialize(self, mode):
+        """Path-kernel builds: 0 (or False) the generic build, 1 the scene-specialised builds, 2 (or
+        True, the default) those plus the lean three-waves-per-SIMD build of throughput-bound
+        launches; identical results (nart_hip_set_specialize)."""
+        self._check(self._lib.nart_hip_set_specialize(self._ctx, int(mode) if not isinstance(mode, bool)
+                                                      else (2 if mode else 0)))
 
     def scene_features(self):
         """(the scene's feature mask, the mask of the path-kernel build the last render launched;

@@ -1141,9 +1141,17 @@ NHD size_t rq_lds_bytes(uint32_t stack_depth, uint32_t block) {
 #endif
 // The counter pass (COUNT: untimed, its counts are per ray and do not depend on the schedule) runs
 // 256-lane blocks at one wave per SIMD, so its counters do not push the kernel past 256 VGPRs.
-#define RQ_BLOCK_OF(COUNT) ((COUNT) ? 256 : NART_RQ_BLOCK)
-template <bool EXT, bool COUNT, bool ENV, uint32_t FM = FT_ALL>
-__global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) void k_render_rq(DScene S, RenderArgs A) {
+//
+// WV = 3: the lean throughput build for launches of >= 3 rounds of resident waves (whole frames),
+// which never use priority lanes or speculative pairs: that code and its state compiled out, 768-lane
+// blocks (12 waves per CU) at three waves per SIMD; only for scenes whose specialised build fits
+// 168 VGPRs and whose traversal stack fits the block's LDS (render.hip lean_fits).
+#define RQ_BLOCK_OF(COUNT, WV) ((COUNT) ? 256 : ((WV) == 3 ? 768 : NART_RQ_BLOCK))
+template <bool EXT, bool COUNT, bool ENV, uint32_t FM = FT_ALL, int WV = 2>
+__global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : NART_RENDER_WAVES)) void k_render_rq(DScene S, RenderArgs A) {
+    // priority lanes, speculative groups and raised issue priority: small-shard schedules only
+    const uint32_t rq_prio = WV == 3 ? 0u : A.rq_prio, rq_pairs = WV == 3 ? 0u : A.rq_pairs;
+    const uint32_t rq_setprio = WV == 3 ? 0u : A.rq_setprio;
     extern __shared__ __attribute__((aligned(16))) int s_dyn[];
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6;
@@ -1196,10 +1204,10 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
     float2 c_sm = make_float2(0.f, 0.f);
     auto take_pixel = [&](uint32_t sl) {
         c_s = 0xFFFFFFFFu;
-        prio = A.rq_prio && (sl & RQ_PRIO_BIT);
-        pm = A.rq_pairs && (sl & RQ_PAIR_BIT);
-        pQ = (A.rq_pairs && (sl & RQ_QUAD_BIT)) ? 4u : (A.rq_pairs ? A.rq_pairs : 1u);
-        if (A.rq_prio) sl &= ~(RQ_PRIO_BIT | RQ_PAIR_BIT | RQ_QUAD_BIT);
+        prio = rq_prio && (sl & RQ_PRIO_BIT);
+        pm = rq_pairs && (sl & RQ_PAIR_BIT);
+        pQ = (rq_pairs && (sl & RQ_QUAD_BIT)) ? 4u : (rq_pairs ? rq_pairs : 1u);
+        if (rq_prio) sl &= ~(RQ_PRIO_BIT | RQ_PAIR_BIT | RQ_QUAD_BIT);
         slot = sl;
         const uint32_t xy = A.slot_xy[sl];
         px = xy & 0xFFFFu;
@@ -1346,7 +1354,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
         // ---------------- path phase
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         newk = 0;
-        if (A.rq_setprio) {
+        if (rq_setprio) {
             const bool want = __ballot(prio && (pm || waiting || s < A.spp)) != 0;
             if (want != raised) {
                 if (want) __builtin_amdgcn_s_setprio(2);
@@ -1399,7 +1407,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
         // shuffles inside the group) and keeps its own record.  Jobs in flight always cover a
         // contiguous run of samples [pF, hs]; a job becomes verified when it reaches the frontier
         // with the frontier's true start state, otherwise every job of the run is dropped.
-        if (A.rq_pairs) {
+        if (rq_pairs) {
             const uint32_t Q = pQ, gb = (uint32_t)lane & ~(Q - 1u), mi = (uint32_t)lane & (Q - 1u);
             const uint32_t NONE = A.spp;
             uint32_t gs[4], gst[4], gfl[4], gend[4], gnd[4];
@@ -1789,7 +1797,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
                 s_nring[(nt + rank) & (RQ_RING - 1u)] = (uint8_t)(lane | (k << 6));
             }
             nt += (uint32_t)__popcll(m);
-            if (A.rq_prio) {
+            if (rq_prio) {
                 const uint64_t mp = __ballot(wp);
                 if (wp) {
                     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mp >> 32),
@@ -1879,7 +1887,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT), COUNT ? 1 : NART_RENDER_WAVES) 
             // -- more path phases, each costing the union of the wave's shading branches; and letting
             // the other lanes sit out the path phases the priority rule starts unless 8 / 24 / 64 of
             // them are ready: 89.9 / 91.0 / 94.4 vs 88.9 ms)
-            if (A.rq_prio && ph == pt && __ballot(tracing && tr_prio) == 0 && __ballot(waiting && prio) != 0) break;
+            if (rq_prio && ph == pt && __ballot(tracing && tr_prio) == 0 && __ballot(waiting && prio) != 0) break;
 
             if (ph == pt && nh == nt && (uint32_t)__popcll(__ballot(tracing)) <= A.rq_quorum) break;
         }

@@ -36,6 +36,7 @@ struct nart_ctx {
     uint32_t features = FT_ALL;  // scene feature mask (scene_features): selects the k_render_rq build
     bool specialize = true;      // nart_hip_set_specialize: scene-specialised path kernels
     uint32_t fm_used = FT_ALL;   // the feature mask of the last path-kernel build launched
+    bool lean = true;            // the three-waves-per-SIMD build where it fits (lean_fits)
     // scene buffers
     void* d_nodes = nullptr;
     void* d_tri_isect = nullptr;
@@ -668,11 +669,11 @@ int sort_groups_by_cost(nart_ctx* ctx, uint32_t n, uint32_t* out, hipStream_t st
     return NART_OK;
 }
 
-template <bool EXT, bool COUNT, bool ENV, uint32_t FM = FT_ALL>
+template <bool EXT, bool COUNT, bool ENV, uint32_t FM = FT_ALL, int WV = 2>
 int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
     auto kern = k_render<EXT, COUNT, ENV>;
-    auto kern_rq = k_render_rq<EXT, COUNT, ENV, FM>;
-    constexpr uint32_t RQB = RQ_BLOCK_OF(COUNT);  // ray-queue block (kernels.h)
+    auto kern_rq = k_render_rq<EXT, COUNT, ENV, FM, WV>;
+    constexpr uint32_t RQB = RQ_BLOCK_OF(COUNT, WV);  // ray-queue block (kernels.h)
     RenderArgs a = a_in;
     if (EXT) {
         // the dielectric list's entries beyond ILIST_REG: one column per thread of the largest
@@ -704,6 +705,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
     const bool rq = ctx->variant == 0 && rq_fits(ctx);
     ctx->fm_used = rq ? FM : FT_ALL;
     if (rq && FM != FT_ALL) ctx->sched |= NART_SCHED_SPECIALIZED;
+    if (rq && WV == 3) ctx->sched |= NART_SCHED_LEAN;
     // camera rays first, coherently (k_primary); NART_PRIMARY=0 leaves them to the path kernel
     const bool primary = !std::getenv("NART_PRIMARY") || std::atoi(std::getenv("NART_PRIMARY")) != 0;
 
@@ -732,7 +734,8 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
         ctx->sched |= NART_SCHED_PRIMARY;
         brq.prim = ctx->d_prim;
     }
-    brq.lds_nodes = render_lds_nodes(ctx, rq_lds_bytes(ctx->stack_depth, RQB), RQB / 256);
+    // one ray-queue block per CU (2 or 3 waves per SIMD)
+    brq.lds_nodes = render_lds_nodes(ctx, rq_lds_bytes(ctx->stack_depth, RQB), NART_RENDER_WAVES);
     const size_t lds_rq = rq_lds_bytes(ctx->stack_depth, RQB) + node_lds_bytes(brq.lds_nodes);
     const dim3 block(256);
     uint32_t blocks = (a.n_slots + 255) / 256;
@@ -884,7 +887,8 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
                 // NART_RQ_PAIRS: lanes per costly pixel (0 off; 1 or 2 pairs; 4 groups of four)
                 const int pe = std::getenv("NART_RQ_PAIRS") ? std::atoi(std::getenv("NART_RQ_PAIRS")) : NART_RQ_GROUP_LANES;
                 const uint32_t Q = pe <= 0 ? 0u : (pe >= 4 ? 4u : 2u);
-                const uint32_t pbit = (rq && prio_on) ? RQ_PRIO_BIT : 0u;
+                // (the lean build has no priority lanes: it runs only where prio_on is false anyway)
+                const uint32_t pbit = (rq && prio_on && WV != 3) ? RQ_PRIO_BIT : 0u;
                 const uint32_t pairs = (pbit && Q && Q * k <= 64u) ? Q : 0u;
                 // NART_RQ_QUAD (A/B): each first-round wave's costliest pixel gets four lanes
                 const bool quad = pbit && pairs == 2u && 2u * k + 2u <= 64u && std::getenv("NART_RQ_QUAD") &&
@@ -945,11 +949,35 @@ constexpr uint32_t FM_DIFFUSE = FT_LAMBERT | FT_DISK;
 constexpr uint32_t FM_GLASS = FT_LAMBERT | FT_GLASS | FT_DISK;
 constexpr uint32_t FM_ENVTEX = FT_LAMBERT | FT_PLASTIC | FT_ENV | FT_TEX | FT_NMAP;
 
+// Rounds of resident waves a launch of n slots spans (launch_render's R): from 3 on the launch is
+// throughput-bound and runs without priority lanes or speculative pairs.
+double launch_rounds(nart_ctx* ctx, uint32_t n) {
+    int cus = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) return 0.0;
+    const size_t lds = (size_t)ctx->stack_depth * 256 * 8 + node_lds_bytes(render_lds_nodes(ctx));
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_render<false, false, false>, 256, lds) !=
+        hipSuccess)
+        return 0.0;
+    const double W = (double)std::max(1, cus * std::max(per_cu, 1)) * 4.0;
+    return (double)n / (64.0 * W);
+}
+
+// The lean three-waves-per-SIMD build (kernels.h WV = 3): throughput-bound launches whose ray-queue
+// LDS fits a 768-lane block (stack depth <= 10 with the top BVH nodes after it)
+bool lean_fits(nart_ctx* ctx, const RenderArgs& a) {
+    if (ctx->variant != 0 || !ctx->lean) return false;
+    if (rq_lds_bytes(ctx->stack_depth, 768) > (size_t)160 * 1024) return false;
+    return launch_rounds(ctx, a.n_slots) >= 3.0;
+}
+
 int dispatch_megakernel(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     const uint32_t f = ctx->features;
     auto covers = [f](uint32_t m) { return (f & ~m) == 0u; };
     if (ctx->specialize && !ctx->counters && a.bounces <= ILIST_REG) {
-        if (!ctx->has_env && covers(FM_DIFFUSE)) return launch_render<false, false, false, FM_DIFFUSE>(ctx, a, st);
+        if (!ctx->has_env && covers(FM_DIFFUSE)) {
+            if (lean_fits(ctx, a)) return launch_render<false, false, false, FM_DIFFUSE, 3>(ctx, a, st);
+            return launch_render<false, false, false, FM_DIFFUSE>(ctx, a, st);
+        }
         if (!ctx->has_env && covers(FM_GLASS)) return launch_render<false, false, false, FM_GLASS>(ctx, a, st);
         if (ctx->has_env && covers(FM_ENVTEX)) return launch_render<false, false, true, FM_ENVTEX>(ctx, a, st);
     }
@@ -1909,10 +1937,14 @@ int nart_hip_set_splat_mode(nart_ctx* ctx, int mode) {
     return NART_OK;
 }
 
-int nart_hip_set_specialize(nart_ctx* ctx, int enable) {
-    if (!ctx) return NART_E_INVALID;
-    ctx->specialize = enable != 0;
-    for (nart_ctx* c : ctx->subs) c->specialize = ctx->specialize;
+int nart_hip_set_specialize(nart_ctx* ctx, int mode) {
+    if (!ctx || mode < 0 || mode > 2) return NART_E_INVALID;
+    ctx->specialize = mode != 0;
+    ctx->lean = mode == 2;
+    for (nart_ctx* c : ctx->subs) {
+        c->specialize = ctx->specialize;
+        c->lean = ctx->lean;
+    }
     return NART_OK;
 }
 

@@ -74,6 +74,14 @@ def test_cornell_specialised(gpu, cornell_scene):
     assert _same_bits(a, b)
 
 
+def test_cornell_lean_build(gpu, cornell_scene):
+    """A throughput-bound Cornell frame (>= 3 rounds of resident waves) runs the lean build: no
+    priority lanes or speculative pairs, 768-lane blocks at three waves per SIMD (kernels.h WV)."""
+    a, b, feats, build, sched = _both(cornell_scene, _params(cornell_scene, 1280, 720, 2))
+    assert build == FM_DIFFUSE and "lean" in sched, (hex(build), sched)
+    assert _same_bits(a, b)
+
+
 def test_c4_specialised(gpu, c4_scene):
     a, b, feats, build, _ = _both(c4_scene, _params(c4_scene, 384, 216, 4))
     assert feats == FM_ENVTEX and build == FM_ENVTEX, (hex(feats), hex(build))

@@ -19,7 +19,7 @@ def main():
     ap.add_argument("-H", type=int, default=1080)
     ap.add_argument("-s", type=int, default=16)
     ap.add_argument("--counters", action="store_true")
-    ap.add_argument("--generic", action="store_true", help="the generic path-kernel build (no scene specialisation)")
+    ap.add_argument("--spec", type=int, default=2, help="path-kernel builds: 0 generic, 1 specialised, 2 + lean")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--bounces", type=int, default=0, help="override the scene's bounce limit")
     ap.add_argument("--env", type=int, default=1024, help="c4: environment map width (height = width / 2)")
@@ -47,8 +47,7 @@ def main():
     if a.bounces:
         p.bounces = a.bounces
     r = nart_amd.HipRenderer(scene)
-    if a.generic:
-        r.set_specialize(False)
+    r.set_specialize(a.spec)
     for rep in range(a.reps):
         st = nart_amd.RenderStats()
         t = time.time()

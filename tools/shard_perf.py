@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--rank", type=int, default=-1, help="-1: every rank of each N (all reported, worst and spread)")
     ap.add_argument("--config", default="c3", help="bench.py config (c2, c3, c4, c5); -s overrides its spp")
-    ap.add_argument("--generic", action="store_true", help="the generic path-kernel build (no scene specialisation)")
+    ap.add_argument("--spec", type=int, default=2, help="path-kernel builds: 0 generic, 1 specialised, 2 + lean")
     a = ap.parse_args()
     sys.path.insert(0, REPO)
     import bench
@@ -42,8 +42,7 @@ def main():
     nb = g.n_buckets_x * g.n_buckets_y
     tpx = g.tile_size * g.tile_size
     gpu = nart_amd.HipRenderer(scene, device=0)
-    if a.generic:
-        gpu.set_specialize(False)
+    gpu.set_specialize(a.spec)
     stream = torch.cuda.current_stream()
     dev = torch.device("cuda", 0)
     for n in a.ns:
