@@ -81,7 +81,11 @@ def build_hip_lib(force=False):
     if not force and _newer(out, srcs):
         return out
     extra = os.environ.get("NART_HIP_DEFINES", "").split()  # development builds, e.g. -DNART_WAVEPROF
-    _run([hipcc(), "--offload-arch=" + ARCH, "-fhip-fp32-correctly-rounded-divide-sqrt"] + COMMON + extra +
+    # -fno-slp-vectorize: no packed-f32 pairs (v_pk_mul_f32 ...) -- their aligned register pairs
+    # raised the ray-queue kernel's register peak (C3 build 230 -> 207 VGPRs without them); the
+    # same IEEE operations either way
+    _run([hipcc(), "--offload-arch=" + ARCH, "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize"] +
+         COMMON + extra +
          ["-shared", "-o", out, os.path.join(CSRC, "render.hip"), os.path.join(CSRC, "host", "bvh_build.cpp"),
           "-L" + LIB, "-lnart_scene", "-Wl,-rpath,$ORIGIN"])
     return out

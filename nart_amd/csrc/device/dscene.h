@@ -147,6 +147,9 @@ struct DScene {
     const uint32_t* tri_mesh;
     const DMesh* meshes;
     const DMaterial* mats;
+    // [mesh] bxdf_eta of the one-lobe BSDF a hit on the mesh creates when the material's patterns
+    // are constant: 0 (Lambert) or the material's eta (kernels.h IList COMPACT)
+    const float* mesh_eta;
     const DLight* lights;
     const DTexture* texs;
     const uint16_t* tex_pool;

@@ -21,24 +21,35 @@ namespace nd {
 #define ILIST_MAX 32
 // this lane's overflow column (formed at each use: no registers held across the kernel)
 #define ILIST_X(A) (EXT ? (A).ilist_ext + (blockIdx.x * blockDim.x + threadIdx.x) : nullptr)
-template <bool EXT>
+// COMPACT (scenes without textures or plastic: kernels built for such a feature mask): an entry's
+// eta is not stored.  Every eta the list receives is bxdf_eta of the BSDF created at a hit on the
+// entry's own mesh (the continuation's or the stepped-through interface's lobe, pathintegrator.cpp:
+// 199-229), and for a one-lobe BSDF with constant patterns that is a per-mesh constant: 0 for
+// Lambert, the material's eta otherwise (DScene::mesh_eta, built on the host from the same
+// floats).  The list then holds 11 registers instead of 21, the same values in the same order.
+template <bool EXT, bool COMPACT = false>
 struct IList {
     uint32_t id[ILIST_REG];  // meshID (24 bit) | priority << 24
-    float eta[ILIST_REG];
+    float eta[COMPACT ? 1 : ILIST_REG];
     uint32_t n;
 
-    ND bool valid(uint32_t meshID, uint32_t prio, float& eta_outer, const uint2* x, uint32_t xs) const {
+    ND bool valid(uint32_t meshID, uint32_t prio, float& eta_outer, const uint2* x, uint32_t xs,
+                  const float* me = nullptr) const {
+        static_assert(!(EXT && COMPACT), "the compact list has no overflow column");
         eta_outer = 1.f;
-        uint32_t lastId = 0;
+        uint32_t lastId = 0, penId = 0;
         float lastEta = 1.f, penEta = 1.f;
         bool ok = true;
 #pragma unroll
         for (int k = 0; k < ILIST_REG; ++k) {
             if (k + 1 == (int)n) {
                 lastId = id[k] & 0xFFFFFFu;
-                lastEta = eta[k];
+                if (!COMPACT) lastEta = eta[k];
             }
-            if (k + 2 == (int)n) penEta = eta[k];
+            if (k + 2 == (int)n) {
+                if (COMPACT) penId = id[k] & 0xFFFFFFu;
+                else penEta = eta[k];
+            }
             if (k < (int)n && (prio & 0xFFu) < (id[k] >> 24)) ok = false;
         }
         if (EXT && n > ILIST_REG) {
@@ -53,8 +64,8 @@ struct IList {
             }
         }
         if (n) {
-            if (lastId != meshID) eta_outer = lastEta;
-            else if (n >= 2) eta_outer = penEta;
+            if (lastId != meshID) eta_outer = COMPACT ? me[lastId] : lastEta;
+            else if (n >= 2) eta_outer = COMPACT ? me[penId] : penEta;
         }
         return ok;
     }
@@ -72,7 +83,7 @@ struct IList {
             for (int j = 0; j + 1 < ILIST_REG; ++j) {
                 if (j >= found && j + 1 < (int)n) {
                     id[j] = id[j + 1];
-                    eta[j] = eta[j + 1];
+                    if (!COMPACT) eta[j] = eta[j + 1];
                 }
             }
             if (EXT && n > ILIST_REG) {
@@ -90,7 +101,7 @@ struct IList {
             for (int k = 0; k < ILIST_REG; ++k) {
                 if (k == (int)n) {
                     id[k] = (meshID & 0xFFFFFFu) | ((prio & 0xFFu) << 24);
-                    eta[k] = eta_s;
+                    if (!COMPACT) eta[k] = eta_s;
                 }
             }
             if (EXT && n >= ILIST_REG)
@@ -164,6 +175,11 @@ struct RenderArgs {
     // ILIST_REG, [entry - ILIST_REG][lane], ilist_stride lanes (>= the launch's threads)
     uint2* ilist_ext = nullptr;
     uint32_t ilist_stride = 0;
+    // k_render_rq lean build (WV = 3): traversal-stack entries per lane kept in LDS (the LDS layout
+    // uses stack_lds, not stack_depth); entries beyond them in gstack, (stack_depth - stack_lds)
+    // 8-B entries per launched thread, lane-major
+    uint32_t stack_lds = 0;
+    int2* gstack = nullptr;
 };
 #define RQ_PRIO_BIT 0x80000000u
 #define RQ_PAIR_BIT 0x40000000u
@@ -1158,7 +1174,9 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
     const int stride = blockDim.x;
     const uint32_t nwave = blockDim.x / 64;
     int2* s_stack = reinterpret_cast<int2*>(s_dyn);
-    float4* s_out = reinterpret_cast<float4*>(s_stack + A.stack_depth * blockDim.x);  // [wave][kind][lane][2]
+    constexpr bool SHORT = WV == 3;  // short LDS stack (RenderArgs::stack_lds)
+    const uint32_t sk = SHORT ? A.stack_lds : A.stack_depth;
+    float4* s_out = reinterpret_cast<float4*>(s_stack + sk * blockDim.x);  // [wave][kind][lane][2]
     uint4* s_res = reinterpret_cast<uint4*>(s_out + nwave * 3 * 64 * 2);             // [wave*64 + lane]
     uint8_t* s_nring = reinterpret_cast<uint8_t*>(s_res + blockDim.x) + wv * 2 * RQ_RING;  // this wave's id rings
     uint8_t* s_pring = s_nring + RQ_RING;
@@ -1170,6 +1188,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
     int* sc = reinterpret_cast<int*>(s_stack + tid);
     const float nL = (float)S.num_lights;
     const uint32_t gid = blockIdx.x * blockDim.x + tid;
+    int2* gstk = SHORT ? A.gstack + (size_t)gid * (A.stack_depth - sk) : nullptr;
 
     uint32_t slot = gid;
     bool gdone = false;  // ghead: no slot group left
@@ -1238,7 +1257,9 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
     f3 c1 = F3(0.f, 0.f, 0.f), c2 = F3(0.f, 0.f, 0.f), betak = F3(0.f, 0.f, 0.f);
     float alpha = 0.f, eta_sampled = 1.f, eta_outer = 1.f, alphaTweak = 1.f;
     uint32_t flags = 0, bounce = 0;
-    IList<EXT> list;
+    // the compact list (no eta registers) where the feature mask allows it
+    constexpr bool CL = !EXT && !(FM & (FT_TEX | FT_PLASTIC));
+    IList<EXT, CL> list;
     list.n = 0;
     bool lightHit = false, use1 = false, use2 = false, have_ed = false, ext_pending = false;
     bool waiting = false;  // rays of this lane's path are queued or in flight
@@ -1593,11 +1614,13 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
             uint32_t gprim = NO_HIT;
             {
                 const uint64_t si = soff + (uint64_t)s * sstr;
-                // (not in the environment-light, deep-list or counter-pass builds, whose registers would spill)
-                if (!ENV && !EXT && !COUNT && s == c_s) {
+                // (not in the environment-light, deep-list, counter-pass or lean builds, whose registers
+                // would spill)
+                constexpr bool PF = !ENV && !EXT && !COUNT && WV != 3;
+                if (PF && s == c_s) {
                     sm = c_sm;
                     gprim = c_prim;
-                } else if (!ENV && !EXT && !COUNT && sstr == 1u && (si & 1u) == 0u && s + 1u < A.spp) {
+                } else if (PF && sstr == 1u && (si & 1u) == 0u && s + 1u < A.spp) {
                     const float4 q = reinterpret_cast<const float4*>(A.samples)[si >> 1];
                     sm = make_float2(q.x, q.y);
                     c_sm = make_float2(q.z, q.w);
@@ -1667,7 +1690,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
             use1 = use2 = false;
             bool cont;
             f3 no, nd;
-            if (list.valid(is.meshID, is.priority, eta_outer, ILIST_X(A), A.ilist_stride)) {
+            if (list.valid(is.meshID, is.priority, eta_outer, ILIST_X(A), A.ilist_stride, S.mesh_eta)) {
                 if (bounce == 0) alpha = 1.f;
                 const f3 wo = to_local(bsdf, neg(cur.d));
                 // ---- EstimateDirect (pathintegrator.cpp:38-121)
@@ -1815,6 +1838,21 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
         // ---------------- traversal phase: lanes take the wave's queued rays in turn
+        if (WV == 3) {
+            // lean build: the traced ray and its slab-test constants are formed again from the ray's
+            // outbox entry (it stays there until the ray resolves) with trav_begin's operations, so
+            // they are not held in registers through the path phase (the old values are dead: the
+            // same bits, 16 fewer registers at the shading peak)
+            if (tracing) {
+                const uint32_t owner = tid8 & 63u, kind = tid8 >> 6;
+                const float4 a = my_out[(kind * 64 + owner) * 2], b = my_out[(kind * 64 + owner) * 2 + 1];
+                tr = make_ray(F3(a.x, a.y, a.z), F3(b.x, b.y, b.z));
+                trav_slab(tr, tq);
+            } else {
+                tr = Ray{};
+                tq.inv = tq.oi = F3(0.f, 0.f, 0.f);
+            }
+        }
 #ifdef NART_WAVEPROF
         const uint64_t prof_tt = __builtin_amdgcn_s_memtime();
         if (cp_on) {
@@ -1851,7 +1889,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
 #ifdef NART_WAVEPROF
                 const uint32_t pn0 = cnt.nodes, pt0 = cnt.tris;
 #endif
-                if (!fin) fin = trav_step<COUNT, ENV && NART_NODE_ROT_ENV>(S, tr, tq, sc, nullptr, stride, cnt, s_nodes, nl);
+                if (!fin) fin = trav_step<COUNT, ENV && NART_NODE_ROT_ENV, SHORT>(S, tr, tq, sc, gstk, stride, cnt, s_nodes, nl, (int)sk);
 #ifdef NART_WAVEPROF
                 if (COUNT && (tid8 >> 6) != 0u) { prof_shn += cnt.nodes - pn0; prof_sht += cnt.tris - pt0; }
 #endif

@@ -142,18 +142,21 @@ struct Trav {
 // best was b >= t* holds no hit below oc_cull(t*).
 ND float oc_cull(const DScene& S, float b) { return b + (b * 0x1p-12f + S.oc_scale * 0x1p-20f); }
 
-ND void trav_begin(const DScene& S, const Ray& r, float tmax, bool ANY, Trav& t) {
-    // Box tests need not be exact (boxes are padded on the host), so use fast reciprocals.
-    // They are clamped to +-1e20: for a zero direction component 1/d = inf would make
-    // fma(lo, inv, -o * inv) = inf - inf = NaN and reject a box the ray runs inside (a camera
-    // ray of the C3 frame has d.z == 0 exactly).  With the clamp the slab distances keep their
-    // signs and stay far beyond any scene distance unless the origin lies within float rounding
-    // of a padded face -- where the box holds no triangle the ray can reach.
+// Box tests need not be exact (boxes are padded on the host), so use fast reciprocals.  They are
+// clamped to +-1e20: for a zero direction component 1/d = inf would make fma(lo, inv, -o * inv) =
+// inf - inf = NaN and reject a box the ray runs inside (a camera ray of the C3 frame has d.z == 0
+// exactly).  With the clamp the slab distances keep their signs and stay far beyond any scene
+// distance unless the origin lies within float rounding of a padded face -- where the box holds no
+// triangle the ray can reach.
+ND void trav_slab(const Ray& r, Trav& t) {
     const float BIG = 1e20f;
     t.inv = F3(fminf(fmaxf(__builtin_amdgcn_rcpf(r.d.x), -BIG), BIG),
                fminf(fmaxf(__builtin_amdgcn_rcpf(r.d.y), -BIG), BIG),
                fminf(fmaxf(__builtin_amdgcn_rcpf(r.d.z), -BIG), BIG));
     t.oi = F3(-r.o.x * t.inv.x, -r.o.y * t.inv.y, -r.o.z * t.inv.z);
+}
+ND void trav_begin(const DScene& S, const Ray& r, float tmax, bool ANY, Trav& t) {
+    trav_slab(r, t);
     t.tmax = tmax;
     t.bestT = tmax;
     t.cullT = ANY ? tmax : oc_cull(S, tmax);
@@ -167,17 +170,29 @@ ND void trav_begin(const DScene& S, const Ray& r, float tmax, bool ANY, Trav& t)
 }
 
 // Traversal stack entry: one 8-B LDS word (node code, entry distance), so a pop is one
-// ds_read_b64 (sc points at this lane's int2 column, laid out [depth][lane]; st is unused).
-// C3 at 64 spp: 134.3 -> 133.9 ms vs two 4-B arrays.
-ND void stk_push(int* sc, float* st, int stride, int sp, int code, float tn) {
-    reinterpret_cast<int2*>(sc)[sp * stride] = make_int2(code, __float_as_int(tn));
+// ds_read_b64 (sc points at this lane's int2 column, laid out [depth][lane]).  C3 at 64 spp:
+// 134.3 -> 133.9 ms vs two 4-B arrays.
+// SHORT (the lean ray-queue build, kernels.h WV = 3): only entries [0, sk) live in LDS; deeper
+// ones go to the lane's own global column gs[sp - sk] (rare: the LDS of a 768-lane block holds
+// too few levels for the deeper BVHs).  The same entries in the same order either way.
+template <bool SHORT = false>
+ND void stk_push(int* sc, int2* gs, int stride, int sp, int code, float tn, int sk = 0) {
+    const int2 v = make_int2(code, __float_as_int(tn));
+    if (!SHORT || sp < sk) reinterpret_cast<int2*>(sc)[sp * stride] = v;
+    else gs[sp - sk] = v;
+}
+template <bool SHORT = false>
+ND int2 stk_read(const int* sc, const int2* gs, int stride, int sp, int sk) {
+    if (!SHORT || sp < sk) return reinterpret_cast<const int2*>(sc)[sp * stride];
+    return gs[sp - sk];
 }
 
 // pop the next subtree that can still contain a closer hit
-ND bool trav_pop(Trav& t, const int* sc, const float* st, int stride) {
+template <bool SHORT = false>
+ND bool trav_pop(Trav& t, const int* sc, const int2* gs, int stride, int sk = 0) {
     while (t.sp > 0) {
         --t.sp;
-        const int2 e = reinterpret_cast<const int2*>(sc)[t.sp * stride];
+        const int2 e = stk_read<SHORT>(sc, gs, stride, t.sp, sk);
         if (__int_as_float(e.y) <= t.cullT) {
             t.code = e.x;
             return true;
@@ -189,15 +204,16 @@ ND bool trav_pop(Trav& t, const int* sc, const float* st, int stride) {
 // trav_pop with its first iteration peeled: the top entry is usually kept, and a lane then pays
 // one LDS read and a compare instead of the loop's exec-mask bookkeeping (the same pops in the
 // same order; C3 316 -> 306 ms, C4 3,287 -> 3,210 ms, profiles/r04z2_pop_peel_ab.log)
-ND bool trav_pop1(Trav& t, const int* sc, const float* st, int stride) {
+template <bool SHORT = false>
+ND bool trav_pop1(Trav& t, const int* sc, const int2* gs, int stride, int sk = 0) {
     if (t.sp <= 0) return false;
     --t.sp;
-    const int2 e = reinterpret_cast<const int2*>(sc)[t.sp * stride];
+    const int2 e = stk_read<SHORT>(sc, gs, stride, t.sp, sk);
     if (__int_as_float(e.y) <= t.cullT) {
         t.code = e.x;
         return true;
     }
-    return trav_pop(t, sc, st, stride);
+    return trav_pop<SHORT>(t, sc, gs, stride, sk);
 }
 
 // One step: descend to the next leaf, test all its triangles, pop the next subtree.  Returns
@@ -235,9 +251,9 @@ NHD inline uint32_t node_quarter(uint32_t i, uint32_t k) {
 #define NART_TRI_PF 2  // triangle records loaded per group in the leaf loop (0: one at a time)
 #endif
 #define NART_TRI_PAD 3  // padding records after tri_perm (a group of up to 4 may read past a leaf)
-template <bool COUNT, bool ROT = false>
-ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, int stride, TraceCounters& cnt,
-                  const float4* lnodes, int nl) {
+template <bool COUNT, bool ROT = false, bool SHORT = false>
+ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, int2* gs, int stride, TraceCounters& cnt,
+                  const float4* lnodes, int nl, int sk = 0) {
     // (a wave-uniform node loop -- ballot per iteration, stopping once at most 0/2/4/8 lanes still
     // descend -- measured 13 % slower in k_render_rq than this per-lane loop: 114 vs 101 ms)
     while (t.code >= 0) {
@@ -313,10 +329,11 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
             // and codes as the branches below (-DNART_TRAV_BRANCH), with fewer exec-mask
             // instructions per node: C3 321 -> 316 ms, 1/8 shard 81 -> 77 ms (profiles/r04t_*)
             const bool both = h0 && h1, swap = n1 < n0;
-            stk_push(sc, st, stride, t.sp, swap ? k.x : k.y, swap ? n0 : n1);
+            // (a short stack's global column is written only when the entry is kept)
+            if (!SHORT || t.sp < sk || both) stk_push<SHORT>(sc, gs, stride, t.sp, swap ? k.x : k.y, swap ? n0 : n1, sk);
             t.sp += both ? 1 : 0;
             t.code = both ? (swap ? k.y : k.x) : (h0 ? k.x : k.y);
-            if (!h0 && !h1 && !trav_pop1(t, sc, st, stride)) return true;
+            if (!h0 && !h1 && !trav_pop1<SHORT>(t, sc, gs, stride, sk)) return true;
             continue;
         }
 #endif
@@ -331,14 +348,14 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
 #else
             bool swap = n1 < n0;
 #endif
-            stk_push(sc, st, stride, t.sp, swap ? k.x : k.y, swap ? n0 : n1);
+            stk_push<SHORT>(sc, gs, stride, t.sp, swap ? k.x : k.y, swap ? n0 : n1, sk);
             ++t.sp;
             t.code = swap ? k.y : k.x;
         } else if (h0) {
             t.code = k.x;
         } else if (h1) {
             t.code = k.y;
-        } else if (!trav_pop(t, sc, st, stride)) {
+        } else if (!trav_pop<SHORT>(t, sc, gs, stride, sk)) {
             return true;
         }
     }
@@ -420,7 +437,7 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, float* st, in
     for (uint32_t i = 0; i < count; ++i)
         if (test(tpp[4 * i], tpp[4 * i + 1], tpp[4 * i + 2], tpp[4 * i + 3])) return true;
 #endif
-    return !trav_pop1(t, sc, st, stride);
+    return !trav_pop1<SHORT>(t, sc, gs, stride, sk);
 }
 
 }  // namespace nd
@@ -436,7 +453,7 @@ ND bool traverse(const DScene& S, const Ray& r, float tmax, bool ANY, float& bes
     Trav t;
     trav_begin(S, r, tmax, ANY, t);
     if (COUNT) WPROF(cnt, 0);
-    while (!trav_step<COUNT>(S, r, t, sc, st, stride, cnt, lnodes, nl)) {
+    while (!trav_step<COUNT>(S, r, t, sc, nullptr, stride, cnt, lnodes, nl)) {
         if (COUNT) WPROF(cnt, 0);
     }
     bestT = t.bestT;

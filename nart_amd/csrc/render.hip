@@ -44,6 +44,7 @@ struct nart_ctx {
     void* d_tris = nullptr;
     void* d_tri_mesh = nullptr;
     void* d_meshes = nullptr;
+    void* d_mesh_eta = nullptr;  // DScene::mesh_eta
     void* d_mats = nullptr;
     void* d_lights = nullptr;
     void* d_texs = nullptr;
@@ -80,6 +81,8 @@ struct nart_ctx {
     uint32_t* d_cost = nullptr;
     void* d_ilist = nullptr;   // dielectric-list columns beyond ILIST_REG (bounces > ILIST_REG)
     size_t cap_ilist = 0;
+    void* d_gstack = nullptr;  // lean build: traversal-stack levels beyond the LDS (RenderArgs::gstack)
+    size_t cap_gstack = 0;
     uint32_t* d_keys[2] = {nullptr, nullptr};
     uint32_t* d_vals[2] = {nullptr, nullptr};
     uint32_t* d_qhead = nullptr;
@@ -669,6 +672,8 @@ int sort_groups_by_cost(nart_ctx* ctx, uint32_t n, uint32_t* out, hipStream_t st
     return NART_OK;
 }
 
+uint32_t lean_stack(const nart_ctx* ctx);
+
 template <bool EXT, bool COUNT, bool ENV, uint32_t FM = FT_ALL, int WV = 2>
 int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
     auto kern = k_render<EXT, COUNT, ENV>;
@@ -734,9 +739,11 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
         ctx->sched |= NART_SCHED_PRIMARY;
         brq.prim = ctx->d_prim;
     }
-    // one ray-queue block per CU (2 or 3 waves per SIMD)
-    brq.lds_nodes = render_lds_nodes(ctx, rq_lds_bytes(ctx->stack_depth, RQB), NART_RENDER_WAVES);
-    const size_t lds_rq = rq_lds_bytes(ctx->stack_depth, RQB) + node_lds_bytes(brq.lds_nodes);
+    // one ray-queue block per CU (2 or 3 waves per SIMD); the lean build keeps lean_stack(ctx)
+    // stack levels in LDS and the rest in a global column per thread
+    const uint32_t skd = WV == 3 ? lean_stack(ctx) : ctx->stack_depth;
+    brq.lds_nodes = render_lds_nodes(ctx, rq_lds_bytes(skd, RQB), NART_RENDER_WAVES);
+    const size_t lds_rq = rq_lds_bytes(skd, RQB) + node_lds_bytes(brq.lds_nodes);
     const dim3 block(256);
     uint32_t blocks = (a.n_slots + 255) / 256;
     const int mode = queue_mode();
@@ -747,7 +754,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
     const uint32_t W = resident * 4;  // resident (persistent) waves
     const double R = (double)a.n_slots / (64.0 * W);  // rounds of resident waves
     // the ray-queue kernel takes kern's place (its own LDS layout); the cost probe keeps k_render
-    auto launch = [&](uint32_t nblocks, const RenderArgs& args) {
+    auto launch = [&](uint32_t nblocks, const RenderArgs& args) -> int {
         if (rq) {
             // traversal-phase quorum: 8 on throughput-bound launches; 0 (every queued ray resolved
             // before the path phase) on small shards, whose costliest pixels' chains set the time
@@ -756,12 +763,34 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
             RenderArgs r2 = args;
             r2.lds_nodes = brq.lds_nodes;
             r2.prim = brq.prim;
+            r2.stack_lds = skd;
             r2.rq_quorum = rqq >= 0 ? (uint32_t)rqq : (R >= q_rounds ? 8u : 0u);
             const uint32_t per = RQB / 256;  // launches are counted in blocks of 256
-            hipLaunchKernelGGL(kern_rq, dim3((nblocks + per - 1) / per), dim3(RQB), lds_rq, st, ctx->scene, r2);
+            const uint32_t grid = (nblocks + per - 1) / per;
+            const size_t threads = (size_t)grid * RQB;
+            if (r2.stack_lds < 1 || r2.stack_lds > ctx->stack_depth || lds_rq > (size_t)160 * 1024)
+                return fail(ctx, NART_E_INVALID, "ray-queue LDS layout out of range");
+            // per-thread global columns, indexed by the global thread id: sized from this grid
+            if (EXT && threads > r2.ilist_stride)
+                return fail(ctx, NART_E_INVALID, "dielectric-list columns smaller than the launch");
+            if (skd < ctx->stack_depth) {
+                const size_t bytes = threads * (ctx->stack_depth - skd) * sizeof(int2);
+                if (bytes > ctx->cap_gstack) {
+                    if (ctx->d_gstack) HIPCHK(hipFree(ctx->d_gstack));
+                    ctx->d_gstack = nullptr;
+                    ctx->cap_gstack = 0;
+                    if (hipMalloc(&ctx->d_gstack, bytes) != hipSuccess)
+                        return fail(ctx, NART_E_OOM, "hipMalloc traversal stack columns");
+                    ctx->cap_gstack = bytes;
+                }
+                r2.gstack = static_cast<int2*>(ctx->d_gstack);
+            }
+            hipLaunchKernelGGL(kern_rq, dim3(grid), dim3(RQB), lds_rq, st, ctx->scene, r2);
         } else {
             hipLaunchKernelGGL(kern, dim3(nblocks), block, lds, st, ctx->scene, args);
         }
+        HIPCHK(hipGetLastError());
+        return NART_OK;
     };
     if (mode > 0) {
         if (blocks > resident) {  // more pixels than resident lanes: persistent grid + queue
@@ -847,9 +876,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
                     // launches are counted in blocks of 256 threads
                     blocks = std::min(blocks, (uint32_t)std::max(1, cus * std::max(per_cu_rq, 1)) * (RQB / 256));
                 }
-                launch(blocks, b);
-                HIPCHK(hipGetLastError());
-                return NART_OK;
+                return launch(blocks, b);
             }
             if (const char* e = std::getenv("NART_QUEUE_K")) k = (uint32_t)std::max(1, std::min(64, std::atoi(e)));
             const bool refill = k < 64u || mode == 1;
@@ -865,9 +892,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
                 size_t tmp = 0;
                 if (k == 64u) {  // whole groups, costliest first (coherent waves, longest chains first)
                     b.queue = ctx->d_queue;
-                    launch(blocks, b);
-                    HIPCHK(hipGetLastError());
-                    return NART_OK;
+                    return launch(blocks, b);
                 }
                 HIPCHK(hipMemcpyAsync(ctx->d_vals[1], ctx->d_cost, (size_t)n * 4, hipMemcpyDeviceToDevice, st));
                 // d_vals[1] = pixels by cost class; partition the rest (slot order) from the top k*W
@@ -924,9 +949,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
             }
         }
     }
-    launch(blocks, b);
-    HIPCHK(hipGetLastError());
-    return NART_OK;
+    return launch(blocks, b);
 }
 
 template <bool ENV>
@@ -949,6 +972,18 @@ constexpr uint32_t FM_DIFFUSE = FT_LAMBERT | FT_DISK;
 constexpr uint32_t FM_GLASS = FT_LAMBERT | FT_GLASS | FT_DISK;
 constexpr uint32_t FM_ENVTEX = FT_LAMBERT | FT_PLASTIC | FT_ENV | FT_TEX | FT_NMAP;
 
+// Traversal-stack levels the lean build keeps in LDS: all of them where the 768-lane block's LDS
+// then still stages NART_LEAN_NODES (default 128) BVH nodes, else as many as leave room for them
+// (>= 4; deeper levels go to per-thread global columns)
+uint32_t lean_stack(const nart_ctx* ctx) {
+    const char* e = std::getenv("NART_LEAN_STACK");
+    if (e) return std::max<uint32_t>(1u, std::min<uint32_t>(ctx->stack_depth, (uint32_t)std::atoi(e)));
+    const size_t nodes = std::min<size_t>(ctx->num_nodes, 128) * sizeof(BVHNode);
+    uint32_t k = ctx->stack_depth;
+    while (k > 4 && rq_lds_bytes(k, 768) + nodes > (size_t)160 * 1024) --k;
+    return k;
+}
+
 // Rounds of resident waves a launch of n slots spans (launch_render's R): from 3 on the launch is
 // throughput-bound and runs without priority lanes or speculative pairs.
 double launch_rounds(nart_ctx* ctx, uint32_t n) {
@@ -965,8 +1000,7 @@ double launch_rounds(nart_ctx* ctx, uint32_t n) {
 // The lean three-waves-per-SIMD build (kernels.h WV = 3): throughput-bound launches whose ray-queue
 // LDS fits a 768-lane block (stack depth <= 10 with the top BVH nodes after it)
 bool lean_fits(nart_ctx* ctx, const RenderArgs& a) {
-    if (ctx->variant != 0 || !ctx->lean) return false;
-    if (rq_lds_bytes(ctx->stack_depth, 768) > (size_t)160 * 1024) return false;
+    if (ctx->variant != 0 || !ctx->lean || !rq_fits(ctx)) return false;
     return launch_rounds(ctx, a.n_slots) >= 3.0;
 }
 
@@ -978,7 +1012,10 @@ int dispatch_megakernel(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             if (lean_fits(ctx, a)) return launch_render<false, false, false, FM_DIFFUSE, 3>(ctx, a, st);
             return launch_render<false, false, false, FM_DIFFUSE>(ctx, a, st);
         }
-        if (!ctx->has_env && covers(FM_GLASS)) return launch_render<false, false, false, FM_GLASS>(ctx, a, st);
+        if (!ctx->has_env && covers(FM_GLASS)) {
+            if (lean_fits(ctx, a)) return launch_render<false, false, false, FM_GLASS, 3>(ctx, a, st);
+            return launch_render<false, false, false, FM_GLASS>(ctx, a, st);
+        }
         if (ctx->has_env && covers(FM_ENVTEX)) return launch_render<false, false, true, FM_ENVTEX>(ctx, a, st);
     }
     return ctx->has_env ? launch_render_maxl<true>(ctx, a, st) : launch_render_maxl<false>(ctx, a, st);
@@ -1800,6 +1837,14 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
         d.normal = dpat(m.normal);
     }
     if ((rc = upload(ctx, ctx->d_mats, mats.data(), mats.size()))) return bail(rc);
+    // per mesh: bxdf_eta of its one-lobe constant-pattern BSDF (the compact dielectric list,
+    // kernels.h IList): B_LAMBERT -> 0, every other one-lobe kind -> the material's eta value
+    std::vector<float> mesh_eta(blob->num_meshes);
+    for (uint32_t m = 0; m < blob->num_meshes; ++m) {
+        const uint32_t mi = blob->meshes[m].material;
+        mesh_eta[m] = (mi >= mats.size() || mats[mi].type == NART_MAT_LAMBERT) ? 0.f : mats[mi].eta.v[0];
+    }
+    if ((rc = upload(ctx, ctx->d_mesh_eta, mesh_eta.data(), mesh_eta.size()))) return bail(rc);
     std::vector<DLight> lights;
     std::vector<DEnvDist> envs;
     for (uint32_t l = 0; l < blob->num_lights; ++l) {
@@ -1839,6 +1884,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     S.tri_mesh = (const uint32_t*)ctx->d_tri_mesh;
     S.meshes = (const DMesh*)ctx->d_meshes;
     S.mats = (const DMaterial*)ctx->d_mats;
+    S.mesh_eta = (const float*)ctx->d_mesh_eta;
     S.lights = (const DLight*)ctx->d_lights;
     S.texs = (const DTexture*)ctx->d_texs;
     S.tex_pool = (const uint16_t*)ctx->d_tex_pool;
@@ -1900,12 +1946,12 @@ void nart_hip_destroy(nart_ctx* ctx) {
         return;
     }
     hipSetDevice(ctx->device);
-    void* bufs[] = {ctx->d_nodes, ctx->d_tri_isect, ctx->d_tri_perm, ctx->d_tris, ctx->d_tri_mesh, ctx->d_meshes, ctx->d_mats,
+    void* bufs[] = {ctx->d_nodes, ctx->d_tri_isect, ctx->d_tri_perm, ctx->d_tris, ctx->d_tri_mesh, ctx->d_meshes, ctx->d_mesh_eta, ctx->d_mats,
                     ctx->d_lights, ctx->d_texs, ctx->d_tex_pool, ctx->d_slot_xy, ctx->d_slot_so, ctx->d_rng, ctx->d_samples, ctx->d_prim,
                     ctx->d_L, ctx->d_bucket_ids, ctx->d_bucket_base, ctx->d_table, ctx->d_lut, ctx->d_counters, ctx->d_envs, ctx->d_density,
                     ctx->d_oc_nodes, ctx->d_oc_chunks, ctx->d_oc_tris, ctx->d_tri_leaf, ctx->d_oc_lock, ctx->d_oc_heap,
                     ctx->d_queue, ctx->d_cost, ctx->d_keys[0], ctx->d_keys[1], ctx->d_vals[0], ctx->d_vals[1],
-                    ctx->d_qhead, ctx->d_sort_tmp, ctx->d_ilist};
+                    ctx->d_qhead, ctx->d_sort_tmp, ctx->d_ilist, ctx->d_gstack};
     for (void* b : bufs)
         if (b) hipFree(b);
     for (void* b : {ctx->d_gather, ctx->d_image})  // nart_hip_render_device's tiles and image

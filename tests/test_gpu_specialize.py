@@ -74,6 +74,18 @@ def test_cornell_specialised(gpu, cornell_scene):
     assert _same_bits(a, b)
 
 
+@pytest.mark.parametrize("lds_levels", [None, "3"], ids=["default", "3-levels"])
+def test_glass_sphere_lean_build(gpu, glass_scene, monkeypatch, lds_levels):
+    """The whole-frame glassSphere launch runs the lean build, whose traversal stack keeps its top
+    levels in LDS and the deeper ones in per-thread global columns (path.h SHORT); with 3 LDS
+    levels most pushes of the 14-level BVH go to the columns.  Same bits as the generic build."""
+    if lds_levels:
+        monkeypatch.setenv("NART_LEAN_STACK", lds_levels)
+    a, b, feats, build, sched = _both(glass_scene, _params(glass_scene, 1280, 720, 2))
+    assert build == FM_GLASS and "lean" in sched, (hex(build), sched)
+    assert _same_bits(a, b)
+
+
 def test_cornell_lean_build(gpu, cornell_scene):
     """A throughput-bound Cornell frame (>= 3 rounds of resident waves) runs the lean build: no
     priority lanes or speculative pairs, 768-lane blocks at three waves per SIMD (kernels.h WV)."""
