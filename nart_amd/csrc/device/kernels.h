@@ -1167,6 +1167,10 @@ template <bool EXT, bool COUNT, bool ENV, uint32_t FM = FT_ALL, int WV = 2>
 __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : NART_RENDER_WAVES)) void k_render_rq(DScene S, RenderArgs A) {
     // priority lanes, speculative groups and raised issue priority: small-shard schedules only
     const uint32_t rq_prio = WV == 3 ? 0u : A.rq_prio, rq_pairs = WV == 3 ? 0u : A.rq_pairs;
+    // a lean build whose shading needs more than Lambert lobes and area lights fits 168 VGPRs only
+    // without the paired sample reads and with the traced ray re-formed per phase (below); the
+    // Lambert-only build keeps both (132 -> 164 VGPRs, still three waves)
+    constexpr bool TIGHT = WV == 3 && (FM & ~(FT_LAMBERT | FT_DISK | FT_RING)) != 0u;
     const uint32_t rq_setprio = WV == 3 ? 0u : A.rq_setprio;
     extern __shared__ __attribute__((aligned(16))) int s_dyn[];
     const int tid = threadIdx.x;
@@ -1616,7 +1620,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
                 const uint64_t si = soff + (uint64_t)s * sstr;
                 // (not in the environment-light, deep-list, counter-pass or lean builds, whose registers
                 // would spill)
-                constexpr bool PF = !ENV && !EXT && !COUNT && WV != 3;
+                constexpr bool PF = !ENV && !EXT && !COUNT && !TIGHT;
                 if (PF && s == c_s) {
                     sm = c_sm;
                     gprim = c_prim;
@@ -1838,7 +1842,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
         // ---------------- traversal phase: lanes take the wave's queued rays in turn
-        if (WV == 3) {
+        if (TIGHT) {
             // lean build: the traced ray and its slab-test constants are formed again from the ray's
             // outbox entry (it stays there until the ray resolves) with trav_begin's operations, so
             // they are not held in registers through the path phase (the old values are dead: the

@@ -973,12 +973,14 @@ constexpr uint32_t FM_GLASS = FT_LAMBERT | FT_GLASS | FT_DISK;
 constexpr uint32_t FM_ENVTEX = FT_LAMBERT | FT_PLASTIC | FT_ENV | FT_TEX | FT_NMAP;
 
 // Traversal-stack levels the lean build keeps in LDS: all of them where the 768-lane block's LDS
-// then still stages NART_LEAN_NODES (default 128) BVH nodes, else as many as leave room for them
-// (>= 4; deeper levels go to per-thread global columns)
+// then still stages 320 BVH nodes (or the whole BVH), else as many as leave room for them (>= 4;
+// deeper levels go to per-thread global columns).  C3 (14 levels, 759 nodes): 8 levels and 352
+// nodes; 7 / 8 / 10 levels measured 241 / 241 / 245 ms per frame, +-7 ms run to run
+// (profiles/r06e_lean_stack_ab.log).  NART_LEAN_STACK (tests) forces a depth.
 uint32_t lean_stack(const nart_ctx* ctx) {
     const char* e = std::getenv("NART_LEAN_STACK");
     if (e) return std::max<uint32_t>(1u, std::min<uint32_t>(ctx->stack_depth, (uint32_t)std::atoi(e)));
-    const size_t nodes = std::min<size_t>(ctx->num_nodes, 128) * sizeof(BVHNode);
+    const size_t nodes = std::min<size_t>(ctx->num_nodes, 320) * sizeof(BVHNode);
     uint32_t k = ctx->stack_depth;
     while (k > 4 && rq_lds_bytes(k, 768) + nodes > (size_t)160 * 1024) --k;
     return k;
