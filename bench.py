@@ -286,12 +286,15 @@ def main():
     by_id = None
     if rank == 0:
         image = torch.zeros((g.total_height, g.total_width, 5), dtype=torch.float32, device=dev)
+        # Render() returns the framebuffer on the host (render.cpp:114-206): each
+        # timed step ends with the combined image copied into this pinned host buffer
+        image_host = torch.empty((g.total_height, g.total_width, 5), dtype=torch.float32, pin_memory=True)
 
-    ev = []  # per step: (start, rendered, gathered) events on the render stream
+    ev = []  # per step: (start, rendered, gathered, combined, on host) events on the render stream
 
     def step(stats):
         nonlocal by_id
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
         e[0].record(stream)
         gpu.render_buckets_async(p, mine, shard.tiles.data_ptr(), stream.cuda_stream, stats)
         e[1].record(stream)
@@ -299,6 +302,12 @@ def main():
         e[2].record(stream)
         if rank == 0:
             gpu.combine_async(p, by_id.data_ptr(), image.data_ptr(), stream.cuda_stream)
+            e[3].record(stream)
+            with torch.cuda.stream(stream):
+                image_host.copy_(image, non_blocking=True)
+        else:
+            e[3].record(stream)
+        e[4].record(stream)
         ev.append(e)
 
     def barrier():
@@ -341,6 +350,7 @@ def main():
     dt = time.perf_counter() - t0
     render_ms = [e[0].elapsed_time(e[1]) for e in ev]
     gather_ms = [e[1].elapsed_time(e[2]) for e in ev]
+    host_copy_ms = [e[3].elapsed_time(e[4]) for e in ev]
     mine_t = torch.tensor([dt, sum(render_ms) / len(ev), sum(gather_ms) / len(ev)], dtype=torch.float64)
     per_rank = [mine_t]
     if dist:
@@ -385,6 +395,12 @@ def main():
                                   if traffic else None),
                 "lane_utilization": prof.get("lane_utilization") if prof else None,
                 "valu_busy": prof.get("valu_busy") if prof else None,
+                # issue-rate ceiling of the path kernel (the limiter that binds):
+                # (SQ_ACTIVE_INST_VALU + SQ_ACTIVE_INST_SALU) / SQ_WAVE_CYCLES per wave (quad-cycle
+                # units: one issue per wave per quad-cycle), times the resident waves per SIMD
+                "issue_frac": prof.get("issue_frac") if prof else None,
+                "issue_frac_wave": prof.get("issue_frac_wave") if prof else None,
+                "waves_per_simd": prof.get("waves_per_simd") if prof else None,
                 "traffic_source": prof_src,
                 "kernel": "k_render_volume_sm" if p.integrator == 1 else "k_primary + k_render_rq",
                 "kernel_avg_ms": round(kernel_avg_ms, 3), "bytes_per_sample": round(bps, 1),
@@ -405,7 +421,7 @@ def main():
         roofline["kernel_split_ms"] = {"k_primary": round(primary_avg_ms, 3),
                                        "k_render_rq": round(kernel_avg_ms - primary_avg_ms, 3)}
     if rank == 0:
-        img_ok = bool(torch.isfinite(image).all().item())
+        img_ok = bool(torch.isfinite(image).all().item()) and bool(torch.equal(image.cpu(), image_host))
         out = {
             "metric": "Msamples/s at %dx%dx%dspp (%s)" % (W, H, SPP, os.path.basename(path)),
             "value": round(value, 3),
@@ -430,6 +446,10 @@ def main():
             "kernel_ms_per_step": round(st.kernel_ms / a.steps, 3),
             "splat_ms_per_step": round(st.splat_ms / a.steps, 3),
             "latin_ms_per_step": round(st.latin_ms / a.steps, 3),
+            "host_copy_ms": round(sum(host_copy_ms) / len(ev), 3),
+            "timing_boundary": "framebuffer on the host: each timed step ends with rank 0's combined float32 image "
+                               "(%d x %d Pixels) copied to pinned host memory (host_copy_ms), as Render() returns "
+                               "std::vector<Pixel> (render.cpp:114-206)" % (g.total_width, g.total_height),
             "image_finite": img_ok,
             "per_rank_ms": [{"rank": r, "step_wall_ms": round(float(v[0]) / a.steps * 1e3, 3),
                              "render_ms": round(float(v[1]), 3), "gather_ms": round(float(v[2]), 3)}

@@ -121,13 +121,10 @@ static_assert(sizeof(OcNode) == 72, "OcNode must be 72 B");
 
 // Scene tables are read-only while a render kernel runs.  cst(p) returns p through the constant
 // address space, so that a read at a wave-uniform index becomes a scalar load (a read at a per-lane
-// index stays a vector load).  -DNART_SCENE_SLOAD=0 keeps plain global reads.
-#ifndef NART_SCENE_SLOAD
-#define NART_SCENE_SLOAD 1
-#endif
+// index stays a vector load).
 template <typename T>
 __host__ __device__ inline const T* cst(const T* p) {
-#if NART_SCENE_SLOAD && defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
     typedef const __attribute__((address_space(4))) T cT;
     return (const T*)(const cT*)(uintptr_t)p;
 #else

@@ -201,9 +201,9 @@ ND size_t sample_index(const RenderArgs& A, uint32_t slot, uint32_t s) {
 }
 
 // Stage the top BVH nodes (breadth-first prefix) into LDS; every thread of the block calls it.
-// With NART_NODE_SWZ the 16-B quarter k of node i sits at quarter (k + (i >> 2)) & 3 of the node's
-// 64 B (node_quarter, path.h), so that the 16-lane groups of a ds_read_b128 spread over all 16
-// bank slots of a 256-B LDS row instead of the 4 that node i mod 4 selects.
+// With ROT the 16-B quarter k of node i sits at quarter (k + (i >> 2)) & 3 of the node's 64 B
+// (node_quarter, path.h), so that the 16-lane groups of a ds_read_b128 spread over all 16 bank
+// slots of a 256-B LDS row instead of the 4 that node i mod 4 selects.
 template <bool ROT = false>
 ND void stage_nodes(const DScene& S, float4* dst, uint32_t n) {
     const float4* src = reinterpret_cast<const float4*>(S.nodes);
@@ -410,12 +410,6 @@ __global__ __launch_bounds__(256) void k_latin_draws(RenderArgs A, LatinScratch 
 #ifndef NART_LATIN_PF
 #define NART_LATIN_PF 16  // choice words (2 swaps each) loaded one batch ahead of their swaps
 #endif
-#ifndef NART_LATIN_PIPE
-#define NART_LATIN_PIPE 0  // 1: swap i+1's reads issued before swap i's writes (register fix-ups)
-#endif
-#ifndef NART_LATIN_HALF
-#define NART_LATIN_HALF 1  // the second half of the shuffle in three-stage batches (k_latin_perm)
-#endif
 __global__ __launch_bounds__(64) void k_latin_perm(RenderArgs A, LatinScratch L) {
     extern __shared__ __attribute__((aligned(16))) uint16_t s_idx[];
     const uint32_t lane = threadIdx.x, g = blockIdx.x;
@@ -432,41 +426,6 @@ __global__ __launch_bounds__(64) void k_latin_perm(RenderArgs A, LatinScratch L)
 #pragma unroll
         for (uint32_t u = 0; u < PF; ++u) cur[u] = c[(size_t)u * 64];
         for (uint32_t i = 0; i < 2 * n2; ++i) ix[i * 64] = (uint16_t)i;
-#if NART_LATIN_PIPE
-        // Reads one swap ahead: swap i+1's two reads are issued before swap i's writes, so each
-        // wait on LDS overlaps the next swap's issue.  LDS executes a wave's operations in order,
-        // so those reads see every write up to swap i-1; swap i's writes (A[i] <- b, A[c_i] <- a)
-        // are applied to them in registers (positions compared, the later write winning).
-        uint32_t pc = cur[0] & 0xFFFFu;             // c_i of the pending reads
-        uint32_t pa = ix[0], pb = ix[pc * 64];      // raw reads of swap i (issued)
-        uint32_t a1 = 0, b1 = 0, c1 = 0xFFFFFFFFu;  // swap i-1: A[c1] <- a1, A[i-1] <- b1
-        for (uint32_t i2 = 0; i2 < n2; i2 += PF) {
-#pragma unroll
-            for (uint32_t u = 0; u < PF; ++u) nxt[u] = i2 + PF + u < n2 ? c[(size_t)(i2 + PF + u) * 64] : 0u;
-#pragma unroll
-            for (uint32_t q = 0; q < 2 * PF; ++q) {
-                const uint32_t i = 2 * i2 + q;
-                if (i < n) {
-                    const uint32_t cn = q + 1 < 2 * PF ? (cur[(q + 1) / 2] >> (16 * ((q + 1) & 1))) & 0xFFFFu
-                                                       : nxt[0] & 0xFFFFu;
-                    const uint32_t in = i + 1 < n ? i + 1 : i;
-                    const uint32_t na = ix[in * 64], nb = ix[(i + 1 < n ? cn : pc) * 64];  // swap i+1's reads
-                    const uint32_t av = c1 == i ? a1 : pa;
-                    const uint32_t bv = pc == c1 ? a1 : (pc + 1u == i ? b1 : pb);
-                    ix[i * 64] = (uint16_t)bv;  // std::swap(A[i], A[c_i]) (sampling.cpp:81-84)
-                    ix[pc * 64] = (uint16_t)av;
-                    a1 = av;
-                    b1 = bv;
-                    c1 = pc;
-                    pa = na;
-                    pb = nb;
-                    pc = cn;
-                }
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < PF; ++u) cur[u] = nxt[u];
-        }
-#else
         // Full batches (all 2*PF swaps valid) load the next batch unconditionally (the choice
         // arrays carry PF padding rows), so that no branch sits between a load and its use: with
         // guarded loads the compiler waited for every outstanding load (vmcnt(0)) before each
@@ -483,7 +442,7 @@ __global__ __launch_bounds__(64) void k_latin_perm(RenderArgs A, LatinScratch L)
         for (; 2 * (i2 + PF) <= n; i2 += PF) {
 #pragma unroll
             for (uint32_t u = 0; u < PF; ++u) nxt[u] = c[(size_t)(i2 + PF + u) * 64];
-            if (NART_LATIN_HALF && 2 * i2 >= m) {  // wave-uniform
+            if (2 * i2 >= m) {  // wave-uniform
                 uint32_t bv[2 * PF], rv[2 * PF];
 #pragma unroll
                 for (uint32_t q = 0; q < 2 * PF; ++q) bv[q] = ix[(2 * i2 + q) * 64];
@@ -527,7 +486,6 @@ __global__ __launch_bounds__(64) void k_latin_perm(RenderArgs A, LatinScratch L)
                 }
             }
         }
-#endif
         for (uint32_t j2 = 0; j2 < n2; ++j2)
             so[(size_t)j2 * 64] = (uint32_t)ix[2 * j2 * 64] | ((uint32_t)ix[(2 * j2 + 1) * 64] << 16);
     }
@@ -546,23 +504,16 @@ ND float latin_value(uint32_t k, uint32_t y, float inv) {
 #ifndef LATIN_EMIT_U
 #define LATIN_EMIT_U 8
 #endif
-#ifndef NART_LATIN_XCD
-#define NART_LATIN_XCD 1
-#endif
 __global__ __launch_bounds__(256) void k_latin_emit(RenderArgs A, LatinScratch L) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_st[];  // [k][p]
     constexpr uint32_t P = LATIN_EMIT_SLOTS, RS = 256 / P, U = LATIN_EMIT_U;
     const uint32_t n = A.spp, n2 = L.n2, t = threadIdx.x, p = t % P;
-#if NART_LATIN_XCD
     // XCD-aware block order: the four blocks whose 16 slots share the 256-B rows of one 64-slot
     // index group are consecutive logical blocks on one XCD (blocks are dealt round robin over the
     // 8 XCDs, each with its own L2), so each row is fetched once instead of once per quarter.
     // Bijective for any grid (cdna_hip_programming.md T1).
     const uint32_t nwg = gridDim.x, q = nwg / 8u, r = nwg % 8u, x = blockIdx.x % 8u;
     const uint32_t bid = (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + blockIdx.x / 8u;
-#else
-    const uint32_t bid = blockIdx.x;
-#endif
     const uint32_t slot = bid * P + p;
     const bool live = slot < A.n_slots;
     const uint32_t* sx = L.sx + latin_row(slot >> 6, n2, 0, slot & 63u);
@@ -632,14 +583,6 @@ enum { ST_EXT = 0, ST_SH1 = 1, ST_SH2 = 2 };
 #ifndef NART_RENDER_WAVES
 #define NART_RENDER_WAVES 2
 #endif
-// development profile: cycles per code section of the path kernel, printed for slot 0
-#ifdef NART_SECTPROF
-#define SECT_T() __builtin_amdgcn_s_memtime()
-#define SECT(i, t) (sect[i] += SECT_T() - (t))
-#else
-#define SECT_T() 0ull
-#define SECT(i, t) ((void)0)
-#endif
 #define NART_RENDER_LB __launch_bounds__(256, NART_RENDER_WAVES)
 // (Round 5: the traversal-quorum form of this kernel -- variant 2/3, C3 whole frame 517 vs 569 ms
 // before the ray-queue kernel replaced it -- was retired; k_render is the cost probe and the
@@ -649,7 +592,6 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
     // LDS traversal stack: stack_depth entries of (node code, entry distance) per lane,
     // laid out [depth][lane] so a wave's 64 lanes hit 64 distinct banks.
     extern __shared__ __attribute__((aligned(16))) int s_dyn[];
-    int* s_code = s_dyn;
     float* s_tn = reinterpret_cast<float*>(s_dyn + A.stack_depth * blockDim.x);
     float4* s_nodes = reinterpret_cast<float4*>(s_dyn + 2 * A.stack_depth * blockDim.x);
     stage_nodes(S, s_nodes, A.lds_nodes);
@@ -701,18 +643,7 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
     bool lightHit = false, use1 = false, use2 = false, cont = false, have_ed = false;
     bool new_sample = true, new_bounce = false;
 
-#ifdef NART_WAVEPROF
-    const uint64_t prof_t0 = __builtin_amdgcn_s_memtime();
-    const bool prof_lead = tid % 64 == 0;
-    uint32_t prof_maxcall = 0;
-    uint64_t prof_iters = 0, prof_trav = 0;
-#endif
-#ifdef NART_SECTPROF
-    uint64_t sect[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const uint64_t sect_t0 = SECT_T();
-#endif
     for (;;) {
-        uint64_t st0 = SECT_T();
         if (A.qhead) {
             // refill lanes whose pixel is done: one queue atomic per wave
             const bool need = new_sample && s >= A.spp;
@@ -749,8 +680,6 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
             new_sample = false;
             new_bounce = true;
         }
-        SECT(0, st0);
-        st0 = SECT_T();
         if (new_bounce) {
             new_bounce = false;
             if (bounce >= A.bounces) {
@@ -784,37 +713,13 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
             stage = ST_EXT;
             if (COUNT) ++n_ext;
         }
-        SECT(1, st0);
-        st0 = SECT_T();
 
         float bt;
         uint32_t bg;
         bool hit;
         {
-#ifdef NART_WAVEPROF
-        const uint64_t prof_t1 = __builtin_amdgcn_s_memtime();
-        const uint32_t prof_n0 = cnt.nodes, prof_t0n = cnt.tris;
-        ++prof_iters;
-#endif
         hit = traverse<COUNT>(S, cur, tmax, stage != ST_EXT, bt, bg, sc, stn, stride, cnt, s_nodes, nl);
-#ifdef NART_WAVEPROF
-        if (COUNT) {
-            const uint32_t dn = cnt.nodes - prof_n0;
-            prof_maxcall = dn > prof_maxcall ? dn : prof_maxcall;
-            if (dn > 1500 && atomicAdd(&A.counters[20], 1ull) < 12)
-                printf("WAVEPROF long query nodes %u tris %u stage %d px (%u,%u) s %u bounce %u o %a %a %a d %a %a %a tmax %a hit %d\n",
-                       dn, cnt.tris - prof_t0n, stage, px, py, s, bounce, cur.o.x, cur.o.y, cur.o.z, cur.d.x, cur.d.y, cur.d.z,
-                       tmax, (int)hit);
-            const uint64_t _e = __ballot(1);
-            const uint64_t dtr = __builtin_amdgcn_s_memtime() - prof_t1;
-            prof_trav += dtr;
-            if ((int)__lane_id() == __builtin_ctzll(_e)) cnt.pw[6] += dtr;
-            if (stage == ST_EXT && hit) WPROF(cnt, 8);
         }
-#endif
-        }
-        SECT(2, st0);
-        st0 = SECT_T();
         bool resolve = false;
         if (stage == ST_EXT) {
             if (!hit) {
@@ -835,8 +740,6 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
             if (list.valid(is.meshID, is.priority, eta_outer, ILIST_X(A), A.ilist_stride)) {
                 if (bounce == 0) alpha = 1.f;
                 const f3 wo = to_local(bsdf, neg(cur.d));
-                SECT(3, st0);
-                st0 = SECT_T();
                 // ---- EstimateDirect (pathintegrator.cpp:38-121)
                 const DLight& Lg = cst(S.lights)[f2u8(gmin(rng_float(rng), ND_ONE_MINUS_EPS) * nL)];
                 float sPdf = 0.f, lPdf = 0.f;
@@ -867,8 +770,6 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
                         }
                     }
                 }
-                SECT(4, st0);
-                st0 = SECT_T();
                 lPdf = 0.f;
                 float lx = rng_float(rng);
                 float ly = rng_float(rng);
@@ -892,8 +793,6 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
                 }
                 betak = beta;
                 have_ed = true;
-                SECT(5, st0);
-                st0 = SECT_T();
                 // ---- continuation (pathintegrator.cpp:199-220)
                 float a = rng_float(rng);
                 float b = rng_float(rng);
@@ -930,7 +829,6 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
                 }
             }
             ++bounce;
-            SECT(6, st0);
             Led = F3(0.f, 0.f, 0.f);
             if (use1) {
                 stage = ST_SH1;
@@ -971,33 +869,6 @@ __global__ NART_RENDER_LB void k_render(DScene S, RenderArgs A) {
             }
         }
     }
-#ifdef NART_SECTPROF
-    sect[7] = SECT_T() - sect_t0;
-    if (slot == 0)
-        printf("SECTPROF new_sample %llu new_bounce %llu traverse %llu isect_bsdf %llu ed_bsdf %llu ed_light %llu cont %llu total %llu\n",
-               (unsigned long long)sect[0], (unsigned long long)sect[1], (unsigned long long)sect[2], (unsigned long long)sect[3],
-               (unsigned long long)sect[4], (unsigned long long)sect[5], (unsigned long long)sect[6], (unsigned long long)sect[7]);
-#endif
-#ifdef NART_WAVEPROF
-    if (COUNT) {
-        if (prof_lead) {
-            const uint64_t dt = __builtin_amdgcn_s_memtime() - prof_t0;
-            cnt.pw[7] += dt;
-            unsigned long long* wv = A.counters + 24 + 8 * (size_t)(gid / 64);
-            wv[0] = dt;
-            wv[3] = slot;
-        }
-        unsigned long long* wv = A.counters + 24 + 8 * (size_t)(gid / 64);
-        if (!A.queue) A.counters[24 + 8 * 70000 + slot] = ((unsigned long long)(n_ext + n_sh) << 32) | cnt.nodes;  // per-slot cost
-        atomicMax(&wv[1], (unsigned long long)prof_trav);  // traversal cycles of the longest lane
-        atomicMax(&wv[2], (unsigned long long)prof_iters); // outer loop iterations of the longest lane
-        atomicAdd(&wv[4], (unsigned long long)cnt.pw[2]);
-        atomicAdd(&wv[5], (unsigned long long)cnt.nodes);
-        atomicAdd(&wv[6], (unsigned long long)cnt.pw[4]);
-        atomicAdd(&wv[7], (unsigned long long)cnt.tris);
-        for (int i = 0; i < 12; ++i) atomicAdd(&A.counters[8 + i], (unsigned long long)cnt.pw[i]);
-    }
-#endif
     if (A.cost) {  // cost probe (one pixel per lane, no queue): node/triangle/iteration weights
         A.cost[gid] = cnt.nodes + 2u * cnt.tris + 30u * iters;
         return;
@@ -1134,8 +1005,6 @@ __global__ __launch_bounds__(256, NART_PRIMARY_WAVES) void k_primary(DScene S, R
 // shard; the frame is unchanged (bit-identical).
 #define RQ_PENDING 0xFFFFFFFEu
 #define RQ_RING 256u
-#define RQ_CHAIN_OFF (24 + 8 * 70000 + 4200000)  // NART_WAVEPROF chain records: 8 words per lane
-#define RQ_CHAIN_MAX 262144u                      // lanes with a record
 NHD size_t rq_lds_bytes(uint32_t stack_depth, uint32_t block) {
     const uint32_t waves = block / 64;
     return (size_t)stack_depth * block * 8 + (size_t)waves * 3 * 64 * 32 + (size_t)block * 16 +
@@ -1148,12 +1017,6 @@ NHD size_t rq_lds_bytes(uint32_t stack_depth, uint32_t block) {
 // 256 faster (132.6 vs 121.5 ms at 64 spp)
 #ifndef NART_RQ_BLOCK
 #define NART_RQ_BLOCK 512
-#endif
-#ifndef NART_ONE_LIGHT
-#define NART_ONE_LIGHT 1  // the single-light EstimateDirect path (k_render_rq)
-#endif
-#ifndef NART_NODE_ROT_ENV
-#define NART_NODE_ROT_ENV 1  // the environment-light builds rotate the LDS node quarters (path.h)
 #endif
 // The counter pass (COUNT: untimed, its counts are per ray and do not depend on the schedule) runs
 // 256-lane blocks at one wave per SIMD, so its counters do not push the kernel past 256 VGPRs.
@@ -1185,7 +1048,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
     uint8_t* s_nring = reinterpret_cast<uint8_t*>(s_res + blockDim.x) + wv * 2 * RQ_RING;  // this wave's id rings
     uint8_t* s_pring = s_nring + RQ_RING;
     float4* s_nodes = reinterpret_cast<float4*>(reinterpret_cast<uint8_t*>(s_res + blockDim.x) + nwave * 2 * RQ_RING);
-    stage_nodes<ENV && NART_NODE_ROT_ENV>(S, s_nodes, A.lds_nodes);
+    stage_nodes<ENV>(S, s_nodes, A.lds_nodes);
     const int nl = (int)A.lds_nodes;
     float4* my_out = s_out + (size_t)wv * 3 * 64 * 2;  // kind k, lane l: my_out[(k * 64 + l) * 2]
     uint4* my_res = s_res + tid;
@@ -1278,30 +1141,6 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
     // wave-uniform ring positions (ids at [pos & (RQ_RING - 1)]): other / priority rays
     uint32_t nh = 0, nt = 0, ph = 0, pt = 0;
 
-#ifdef NART_WAVEPROF
-    const uint64_t prof_t0 = __builtin_amdgcn_s_memtime();
-    const uint64_t prof_rt0 = __builtin_amdgcn_s_memrealtime();
-    uint64_t prof_sec[4] = {0, 0, 0, 0};  // path phase: results + shading, refill, new samples, id lists
-    uint64_t prof_last = prof_t0;
-    uint32_t prof_shn = 0, prof_sht = 0;  // node visits / triangle tests of shadow rays
-#define RQ_MARK(i)                                                 \
-    do {                                                           \
-        const uint64_t _n = __builtin_amdgcn_s_memtime();          \
-        prof_sec[i] += _n - prof_last;                             \
-        prof_last = _n;                                            \
-    } while (0)
-    // critical-path record of the lane's first pixel (its chain): shader cycles with its own rays
-    // in flight, with its rays resolved while the traversal phase serves other lanes, in path
-    // phases where it shaded or started samples, in path phases where it did not, and otherwise
-    // (RQ_CHAIN_OFF records, render.hip prints the last-finishing chains)
-    bool cp_on = slot != 0xFFFFFFFFu;
-    const uint32_t cp_slot = slot;
-    const bool cp_prio = prio, cp_pm = pm;
-    uint64_t cp_tr = 0, cp_wait = 0, cp_shade = 0, cp_other = 0, cp_idle = 0;
-    bool cp_did = false;
-#else
-#define RQ_MARK(i) ((void)0)
-#endif
     auto put_ray = [&](int kind, f3 o, f3 d, float tmax) {
         float4* e = my_out + (kind * 64 + lane) * 2;
         e[0] = make_float4(o.x, o.y, o.z, tmax);
@@ -1339,32 +1178,16 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
         ++nd;
         return rng_float(rng);
     };
-    // a sample's result: written at once, or held by a pair lane until verified
-#ifndef NART_PAIR_WRITES
-#define NART_PAIR_WRITES 0
-#endif
-    // NART_PAIR_WRITES: pixel-major rows keep an even sample's Li_alpha until the odd one after it
-    // and store both as one 32-B access (a lane's consecutive 16-B stores hit a line that was
-    // evicted in between)
-    float4 c_L = make_float4(0.f, 0.f, 0.f, 0.f);
-    bool c_held = false;
+    // a sample's result: written at once, or held by a pair lane until verified.  (Pairing an even
+    // sample's result with the odd one after it as one 32-B store cut the writes 26.6 -> 11.1 GB
+    // per C3 launch but ran 2.3 % slower, profiles/r05j_pair_writes_ab.log; retired in round 6.)
     auto end_sample = [&](float4 v) {
         if (pm) {
             jres = v;
             jend = rng;
             jfl |= J_FIN;
         } else {
-            const uint64_t si = soff + (uint64_t)s * sstr;
-            if (NART_PAIR_WRITES && !ENV && !EXT && !COUNT && c_held) {
-                typedef float v8f __attribute__((ext_vector_type(8)));
-                *reinterpret_cast<v8f*>(A.Lout + (si - 1u)) = v8f{c_L.x, c_L.y, c_L.z, c_L.w, v.x, v.y, v.z, v.w};
-                c_held = false;
-            } else if (NART_PAIR_WRITES && !ENV && !EXT && !COUNT && sstr == 1u && (si & 1u) == 0u && s + 1u < A.spp) {
-                c_L = v;
-                c_held = true;
-            } else {
-                A.Lout[si] = v;
-            }
+            A.Lout[soff + (uint64_t)s * sstr] = v;
             ++s;
         }
     };
@@ -1387,12 +1210,6 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
                 raised = want;
             }
         }
-#ifdef NART_WAVEPROF
-        if (COUNT && lane == 0) cnt.pw[10]++;  // path phases
-        const uint64_t prof_tp = __builtin_amdgcn_s_memtime();
-        prof_last = prof_tp;
-        cp_did = false;
-#endif
         // 1. results of lanes whose queries are all in: EstimateDirect term, then the hit to
         //    shade or the end of the sample
         bool need_shade = false;
@@ -1550,23 +1367,6 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
                 if (pF >= A.spp && all_none && !any_doom) pm = false;
             }
         }
-        RQ_MARK(0);
-#ifdef NART_WAVEPROF
-        if (cp_on && !pm && s >= A.spp && !waiting && gid < RQ_CHAIN_MAX) {
-            // the first pixel's chain is done: its record (the path phase so far counts as its own)
-            cp_shade += __builtin_amdgcn_s_memtime() - prof_tp;
-            unsigned long long* rec = A.counters + RQ_CHAIN_OFF + 8 * (size_t)gid;
-            rec[0] = (unsigned long long)cp_slot | (cp_prio ? 1ull << 32 : 0ull) | (cp_pm ? 1ull << 33 : 0ull) | (1ull << 34);
-            rec[1] = __builtin_amdgcn_s_memrealtime() - prof_rt0;
-            rec[2] = cp_tr;
-            rec[3] = cp_wait;
-            rec[4] = cp_shade;
-            rec[5] = cp_other;
-            rec[6] = cp_idle;
-            rec[7] = __builtin_amdgcn_s_memtime() - prof_t0;
-            cp_on = false;
-        }
-#endif
         // pixel refill (persistent grid): one queue atomic per wave
         if (A.qhead) {
             const bool need = !pm && !waiting && s >= A.spp && slot != 0xFFFFFFFEu;
@@ -1602,14 +1402,10 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
             }
         }
         bool active = !waiting && !need_shade && s < A.spp && !(jfl & J_FIN);
-        RQ_MARK(1);
         // 2. new samples (pathintegrator.cpp:144-166; render.cpp:87-95).  A camera ray that
         //    k_primary found to escape, or a zero bounce limit, ends its sample here, so loop until
         //    a hit is to be shaded, a ray is queued or the pixel is done.
         while (active) {
-#ifdef NART_WAVEPROF
-            cp_did = true;
-#endif
             nd = 0;
             // pixel-major rows (stride 1): samples and camera hits are read in pairs, the odd one
             // kept for the lane's next sample -- each read of a line the lane's neighbours do not
@@ -1677,14 +1473,9 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
             }
             active = false;
         }
-        RQ_MARK(2);
         // 3. shade the hits (pathintegrator.cpp:185-246)
         if (need_shade) {
-#ifdef NART_WAVEPROF
-            cp_did = true;
-#endif
             if (COUNT) ++n_bounce;
-            if (COUNT) WPROF(cnt, 8);
             const float4 ro = my_out[lane * 2], rd = my_out[lane * 2 + 1];
             const Ray cur = make_ray(F3(ro.x, ro.y, ro.z), F3(rd.x, rd.y, rd.z));
             Isect is;
@@ -1704,7 +1495,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
                 // read through a wave-uniform index (scalar loads of the light record and, for an
                 // environment light, its sampling tables): C3 / C2 frames -1.3 %, C4 -0.9 %
                 // (profiles/r05am_one_light_all.log, r05al_c4_one_light_ab.log)
-                const bool one_light = NART_ONE_LIGHT && S.num_lights == 1u;
+                const bool one_light = S.num_lights == 1u;
                 float sPdf = 0.f, lPdf = 0.f;
                 float sx = draw();
                 float sy = draw();
@@ -1834,7 +1625,6 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
                 pt += (uint32_t)__popcll(mp);
             }
         }
-        RQ_MARK(3);
         // a lane whose sample ended while shading starts its next sample in the next phase; one
         // whose pixel is done may still get a pixel from the queue
         const bool more = !waiting && (s < A.spp || pm || (A.qhead && slot != 0xFFFFFFFEu) || (A.ghead && !gdone));
@@ -1857,14 +1647,6 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
                 tq.inv = tq.oi = F3(0.f, 0.f, 0.f);
             }
         }
-#ifdef NART_WAVEPROF
-        const uint64_t prof_tt = __builtin_amdgcn_s_memtime();
-        if (cp_on) {
-            if (cp_did) cp_shade += prof_tt - prof_tp;
-            else cp_other += prof_tt - prof_tp;
-        }
-        uint64_t cp_last = prof_tt;
-#endif
         for (;;) {
             const bool need = !tracing;
             const uint64_t mn = __ballot(need);
@@ -1888,15 +1670,8 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
             }
             bool fin = false;
             if (tracing) {
-                if (COUNT) WPROF(cnt, 0);
                 fin = !S.geometry_visible;  // one-chunk scenes render no geometry (Q14)
-#ifdef NART_WAVEPROF
-                const uint32_t pn0 = cnt.nodes, pt0 = cnt.tris;
-#endif
-                if (!fin) fin = trav_step<COUNT, ENV && NART_NODE_ROT_ENV, SHORT>(S, tr, tq, sc, gstk, stride, cnt, s_nodes, nl, (int)sk);
-#ifdef NART_WAVEPROF
-                if (COUNT && (tid8 >> 6) != 0u) { prof_shn += cnt.nodes - pn0; prof_sht += cnt.tris - pt0; }
-#endif
+                if (!fin) fin = trav_step<COUNT, ENV, SHORT>(S, tr, tq, sc, gstk, stride, cnt, s_nodes, nl, (int)sk);
             }
             if (fin) {
                 tracing = false;
@@ -1909,20 +1684,6 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
                 const uint32_t kind = tid8 >> 6;
                 rw[kind] = kind == 0u ? bg : (bg != NO_HIT ? 1u : 0u);
             }
-#ifdef NART_WAVEPROF
-            if (cp_on) {
-                const uint64_t now = __builtin_amdgcn_s_memtime();
-                if (waiting) {
-                    const uint4 r = *my_res;
-                    const bool in = (!ext_pending || r.x != RQ_PENDING) && (!use1 || r.y != 2u) && (!use2 || r.z != 2u);
-                    if (in) cp_wait += now - cp_last;
-                    else cp_tr += now - cp_last;
-                } else {
-                    cp_idle += now - cp_last;
-                }
-                cp_last = now;
-            }
-#endif
             // priority rays all resolved and a priority lane waits on its results: shade it now (ending
             // the phase as soon as 1/2/4/8 priority lanes were ready, with other priority rays still in
             // flight, measured slower: C3 1/8 shard 121/114/102/94 vs 90 ms, profiles/r05d_rq_early_ab.log
@@ -1933,27 +1694,7 @@ __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : 
 
             if (ph == pt && nh == nt && (uint32_t)__popcll(__ballot(tracing)) <= A.rq_quorum) break;
         }
-#ifdef NART_WAVEPROF
-        if (COUNT && (int)__lane_id() == __builtin_ctzll(__ballot(1))) cnt.pw[6] += __builtin_amdgcn_s_memtime() - prof_tt;
-#endif
     }
-#ifdef NART_WAVEPROF
-    if (COUNT && lane == 0) {
-        // wave timeline (constant-rate global clock): start, end
-        unsigned long long* wvr = A.counters + 24 + 8 * 70000 + 4200000 - 2 * 70000 + 2 * (size_t)(gid / 64);
-        wvr[0] = prof_rt0;
-        wvr[1] = __builtin_amdgcn_s_memrealtime();
-    }
-    if (COUNT) {
-        if (lane == 0) cnt.pw[7] += __builtin_amdgcn_s_memtime() - prof_t0;
-        for (int i = 0; i < 12; ++i) atomicAdd(&A.counters[8 + i], (unsigned long long)cnt.pw[i]);
-        if (lane == 0)
-            for (int i = 0; i < 4; ++i) atomicAdd(&A.counters[24 + 8 * 69999 + i], (unsigned long long)prof_sec[i]);
-        atomicAdd(&A.counters[24 + 8 * 69999 + 4], (unsigned long long)prof_shn);
-        atomicAdd(&A.counters[24 + 8 * 69999 + 5], (unsigned long long)prof_sht);
-    }
-#endif
-#undef RQ_MARK
     if (COUNT) {
         atomicAdd(&A.counters[0], (unsigned long long)n_ext);
         atomicAdd(&A.counters[1], (unsigned long long)n_sh);
@@ -2382,7 +2123,7 @@ __global__ __launch_bounds__(256) void k_splat_skew(SplatArgs A) {
         bh = (int)(min(y0 + A.B, A.totalH) - y0);
         base = A.bucket_base[bi];
     }
-    const float fw = A.fw, fbf = (float)A.fb;
+    const float fw = A.fw;
     const float edgeX = (float)(x0 + A.B + A.fb), edgeY = (float)(y0 + A.B + A.fb);
     // pre-pass: which last-column sources (bit sy) / last-row sources (bit sx) have wrapping samples
     if (live) {

@@ -62,11 +62,6 @@ ND Ray make_ray(f3 o, f3 d) {
 }
 // (p[m0], p[m1], p[major]) permutation of Triangle::Intersect (geometry.cpp:48-56)
 ND f3 permute(f3 p, int major) {  // selects, not branches: major differs across lanes
-#ifdef NART_PERMUTE_BRANCH
-    if (major == 0) return F3(p.y, p.z, p.x);
-    if (major == 1) return F3(p.z, p.x, p.y);
-    return p;
-#endif
     const bool m0 = major == 0, m1 = major == 1;
     return F3(m0 ? p.y : (m1 ? p.z : p.x), m0 ? p.z : (m1 ? p.x : p.y), m0 ? p.x : (m1 ? p.y : p.z));
 }
@@ -96,26 +91,7 @@ ND bool edges_accept(float e0, float e1, float e2) {  // geometry.cpp:78-81
 struct TraceCounters {
     uint32_t nodes, tris;
     uint32_t oc_checks, oc_replays;  // octree.h: exact ancestor checks, octree replays
-#ifdef NART_WAVEPROF
-    // development profile (counter pass only): wave-level iterations and active lanes of the
-    // traversal step / node / triangle loops, cycles in traversal and in total
-    uint64_t pw[12];
-#endif
 };
-#ifdef NART_WAVEPROF
-#define WPROF(cnt, i)                                                  \
-    do {                                                               \
-        const uint64_t _e = __ballot(1);                               \
-        if ((int)__lane_id() == __builtin_ctzll(_e)) {                 \
-            (cnt).pw[i]++;                                             \
-            (cnt).pw[(i) + 1] += (uint64_t)__popcll(_e);               \
-        }                                                              \
-    } while (0)
-#else
-#define WPROF(cnt, i) \
-    do {              \
-    } while (0)
-#endif
 
 // Closest hit (ANY=false): minimum (t, scene index) over triangles with 0 < t < tmax whose
 // sheared edge test passes -- the set Octree::Intersect selects from (bvh.cpp:132-176).
@@ -219,33 +195,18 @@ ND bool trav_pop1(Trav& t, const int* sc, const int2* gs, int stride, int sk = 0
 // One step: descend to the next leaf, test all its triangles, pop the next subtree.  Returns
 // true when the query is resolved (t.bestG = winner or NO_HIT).  (A one-node-or-one-triangle
 // "if-if" step measured slower on C3: 123 vs 95 ms per frame in the wavefront trace kernel.)
-#ifndef NART_NODE_SWZ
-// 1: rotate the quarters of LDS-staged nodes (bank spread): C4 path kernel 52.1 -> 51.3 ms but C3
-// 276.2 -> 279.4 ms (the per-visit address arithmetic), profiles/r05ad_node_swz_ab.txt
-#define NART_NODE_SWZ 0
-#endif
-#ifndef NART_NODE_PAD
-// 1: measured C3 path kernel 276.3 -> 282.5 ms, C4 51.9 -> 51.6 ms (profiles/r05ae_node_pad_ab.txt)
-#define NART_NODE_PAD 0
-#endif
-// LDS-staged nodes: with NART_NODE_PAD a 16-B pad follows every 4 nodes, so that node i starts at
-// 16-B slot (5 i / 4 + ...) mod 16 of a 256-B LDS row: the 16-lane groups of a ds_read_b128 of
-// random nodes spread over all 16 slots instead of the 4 that i mod 4 selects (bank conflicts),
-// for one extra shift-and-add per node visit.  node_slot: first float4 of node i.
-NHD inline uint32_t node_slot(uint32_t i) {
-#if NART_NODE_PAD
-    return 4u * i + (i >> 2);
-#else
-    return 4u * i;
-#endif
-}
-NHD inline size_t node_lds_bytes(uint32_t n) { return (size_t)16 * (n ? node_slot(n - 1u) + 4u : 0u); }
-// LDS quarter of 16-B part k of BVH node i (stage_nodes, kernels.h).  ROT: rotate by (i >> 2) & 3
-// (the environment-light builds, whose larger BVHs gain from the bank spread; NART_NODE_SWZ=1: all)
+// LDS-staged nodes, 64 B each (a 16-B pad after every 4 nodes measured C3 276.3 -> 282.5 ms,
+// C4 51.9 -> 51.6 ms and was retired, profiles/r05ae_node_pad_ab.txt).  node_slot: first float4 of
+// node i.
+NHD uint32_t node_slot(uint32_t i) { return 4u * i; }
+NHD size_t node_lds_bytes(uint32_t n) { return (size_t)16 * (n ? node_slot(n - 1u) + 4u : 0u); }
+// LDS quarter of 16-B part k of BVH node i (stage_nodes, kernels.h).  ROT: rotate by (i >> 2) & 3,
+// in the environment-light builds, whose larger BVHs gain from the bank spread (C4 path kernel
+// 52.1 -> 51.3 ms at 1080p/32; C3 276.2 -> 279.4 ms, so the other builds do not rotate:
+// profiles/r05ad_node_swz_ab.txt, r05aj_c4_node_rot_ab.log)
 template <bool ROT = false>
-NHD inline uint32_t node_quarter(uint32_t i, uint32_t k) {
-    if (ROT || NART_NODE_SWZ) return (k + (i >> 2)) & 3u;
-    return k;
+NHD uint32_t node_quarter(uint32_t i, uint32_t k) {
+    return ROT ? (k + (i >> 2)) & 3u : k;
 }
 #ifndef NART_TRI_PF
 #define NART_TRI_PF 2  // triangle records loaded per group in the leaf loop (0: one at a time)
@@ -258,31 +219,16 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, int2* gs, int
     // descend -- measured 13 % slower in k_render_rq than this per-lane loop: 114 vs 101 ms)
     while (t.code >= 0) {
         if (COUNT) cnt.nodes++;
-        if (COUNT) WPROF(cnt, 2);
         float4 a, b, c;
         int4 k;
-#if defined(NART_LDS_ALL) && defined(__HIP_DEVICE_COMPILE__)
-        // every node staged in LDS (experiment: valid only when the whole BVH fits)
-        if (true) {
-            typedef float v4f __attribute__((ext_vector_type(4)));
-            typedef const __attribute__((address_space(3))) v4f lds_v4f;
-            lds_v4f* np = (lds_v4f*)lnodes + node_slot((uint32_t)t.code);
-            const uint32_t r = node_quarter<ROT>((uint32_t)t.code, 0u);
-            const v4f qa = np[r], qb = np[(r + 1u) & 3u], qc = np[(r + 2u) & 3u], qk = np[(r + 3u) & 3u];
-            a = make_float4(qa.x, qa.y, qa.z, qa.w);
-            b = make_float4(qb.x, qb.y, qb.z, qb.w);
-            c = make_float4(qc.x, qc.y, qc.z, qc.w);
-            k = make_int4(__float_as_int(qk.x), __float_as_int(qk.y), __float_as_int(qk.z), __float_as_int(qk.w));
-        } else
-#endif
         if (t.code < nl) {
-#if !defined(NART_NODE_FLAT) && defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
             // explicit LDS address space: ds_read_b128, not a flat load through the generic aperture.
             // A flat load counts against both the vector-memory and the LDS counters, and the
             // compiler serialised the node's four flat loads behind waits for earlier triangle
             // loads; the LDS loads issue together.  k_render_rq, C3: 346.3 -> 336.5 ms per frame,
             // 1/8 shard 85.9 -> 81.9 ms (profiles/r04_node_ds_ab.log; round 1's k_render measured
-            // 577 vs 570 ms the other way).  -DNART_NODE_FLAT restores the flat load.
+            // 577 vs 570 ms the other way).
             typedef float v4f __attribute__((ext_vector_type(4)));
             typedef const __attribute__((address_space(3))) v4f lds_v4f;
             lds_v4f* np = (lds_v4f*)lnodes + node_slot((uint32_t)t.code);
@@ -321,43 +267,18 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, int2* gs, int
         float f1 = fminf(fminf(fmaxf(ux0, ux1), fmaxf(uy0, uy1)), fmaxf(uz0, uz1));
         bool h0 = (n0 <= f0) && (f0 >= 0.f) && (n0 <= t.cullT);
         bool h1 = (n1 <= f1) && (f1 >= 0.f) && (n1 <= t.cullT);
-#if !defined(NART_TRAV_BRANCH) && !defined(NART_ORDER)
-        {
-            // the child choice as selects: the far child is written to the free slot at sp on
-            // every step and kept (sp + 1) only when both children are entered (sp <= max_stack <
-            // stack_depth, so the write stays inside the lane's stack); the same entries, order
-            // and codes as the branches below (-DNART_TRAV_BRANCH), with fewer exec-mask
-            // instructions per node: C3 321 -> 316 ms, 1/8 shard 81 -> 77 ms (profiles/r04t_*)
-            const bool both = h0 && h1, swap = n1 < n0;
-            // (a short stack's global column is written only when the entry is kept)
-            if (!SHORT || t.sp < sk || both) stk_push<SHORT>(sc, gs, stride, t.sp, swap ? k.x : k.y, swap ? n0 : n1, sk);
-            t.sp += both ? 1 : 0;
-            t.code = both ? (swap ? k.y : k.x) : (h0 ? k.x : k.y);
-            if (!h0 && !h1 && !trav_pop1<SHORT>(t, sc, gs, stride, sk)) return true;
-            continue;
-        }
-#endif
-        if (h0 && h1) {
-#if defined(NART_ORDER) && NART_ORDER == 1
-            // entry distances clamped to the origin; ties (both boxes hold the origin) by exit
-            const float k0 = fmaxf(n0, 0.f), k1 = fmaxf(n1, 0.f);
-            bool swap = k1 < k0 || (k1 == k0 && f1 < f0);
-#elif defined(NART_ORDER) && NART_ORDER == 2
-            const float k0 = fmaxf(n0, 0.f), k1 = fmaxf(n1, 0.f);
-            bool swap = k1 < k0 || (k1 == k0 && f1 > f0);
-#else
-            bool swap = n1 < n0;
-#endif
-            stk_push<SHORT>(sc, gs, stride, t.sp, swap ? k.x : k.y, swap ? n0 : n1, sk);
-            ++t.sp;
-            t.code = swap ? k.y : k.x;
-        } else if (h0) {
-            t.code = k.x;
-        } else if (h1) {
-            t.code = k.y;
-        } else if (!trav_pop<SHORT>(t, sc, gs, stride, sk)) {
-            return true;
-        }
+        // the child choice as selects: the far child is written to the free slot at sp on every step
+        // and kept (sp + 1) only when both children are entered (sp <= max_stack < stack_depth, so
+        // the write stays inside the lane's stack); the nearer child (by entry distance) first.
+        // Against the branch form (push when both, else take the one hit, else pop): the same
+        // entries, order and codes with fewer exec-mask instructions per node: C3 321 -> 316 ms,
+        // 1/8 shard 81 -> 77 ms (profiles/r04t_*)
+        const bool both = h0 && h1, swap = n1 < n0;
+        // (a short stack's global column is written only when the entry is kept)
+        if (!SHORT || t.sp < sk || both) stk_push<SHORT>(sc, gs, stride, t.sp, swap ? k.x : k.y, swap ? n0 : n1, sk);
+        t.sp += both ? 1 : 0;
+        t.code = both ? (swap ? k.y : k.x) : (h0 ? k.x : k.y);
+        if (!h0 && !h1 && !trav_pop1<SHORT>(t, sc, gs, stride, sk)) return true;
     }
     const uint32_t lc = ~(uint32_t)t.code;
     const uint32_t first = lc >> 5, count = (lc & 31u) + 1u;
@@ -370,7 +291,6 @@ ND bool trav_step(const DScene& S, const Ray& r, Trav& t, int* sc, int2* gs, int
     // any-hit query is answered
     auto test = [&](const float4 b, const float4 c, const float4 dd, const float4 a) -> bool {
         if (COUNT) cnt.tris++;
-        if (COUNT) WPROF(cnt, 4);
         f3 p0 = F3(b.x - op.x, b.y - op.y, b.z - op.z);
         f3 p1 = F3(b.w - op.x, c.x - op.y, c.y - op.z);
         f3 p2 = F3(c.z - op.x, c.w - op.y, dd.x - op.z);
@@ -452,9 +372,7 @@ ND bool traverse(const DScene& S, const Ray& r, float tmax, bool ANY, float& bes
     if (!S.geometry_visible) return false;
     Trav t;
     trav_begin(S, r, tmax, ANY, t);
-    if (COUNT) WPROF(cnt, 0);
     while (!trav_step<COUNT>(S, r, t, sc, nullptr, stride, cnt, lnodes, nl)) {
-        if (COUNT) WPROF(cnt, 0);
     }
     bestT = t.bestT;
     bestG = t.bestG;
@@ -473,9 +391,6 @@ ND bool traverse(const DScene& S, const Ray& r, float tmax, bool ANY, float& bes
 // hit and risky flags the same ties and NaNs or more -- so oc_resolve returns the reference octree's
 // answer as after traverse() (path.h trav_step, octree.h).  wstk: this wave's LDS stack, 16 B per
 // level.
-#ifndef NART_PACKET_SLOAD
-#define NART_PACKET_SLOAD 1
-#endif
 template <bool COUNT>
 ND void traverse_packet(const DScene& S, const Ray& r, float tmax, float& bestT, uint32_t& bestG, uint4* wstk,
                         TraceCounters& cnt) {
@@ -489,15 +404,12 @@ ND void traverse_packet(const DScene& S, const Ray& r, float tmax, float& bestT,
     uint64_t mask = __ballot(1);
     int sp = 0;
     const f3 op = permute(r.o, r.major);
-#if NART_PACKET_SLOAD
     const int maj0 = __builtin_amdgcn_readfirstlane(r.major);
     const bool umaj = __ballot(r.major != maj0) == 0;
-#endif
     for (;;) {
         const bool in = (mask >> me) & 1ull;
         bool pop = false;
         if (code >= 0) {
-#if NART_PACKET_SLOAD
             // code is wave-uniform: the node is read through the constant address space, i.e. as
             // one scalar load (the node array is not written while a render kernel runs)
             typedef float v4f __attribute__((ext_vector_type(4)));
@@ -507,11 +419,6 @@ ND void traverse_packet(const DScene& S, const Ray& r, float tmax, float& bestT,
             const float4 a = make_float4(qa.x, qa.y, qa.z, qa.w), b = make_float4(qb.x, qb.y, qb.z, qb.w),
                          c = make_float4(qc.x, qc.y, qc.z, qc.w);
             const int4 k = make_int4(__float_as_int(qk.x), __float_as_int(qk.y), __float_as_int(qk.z), __float_as_int(qk.w));
-#else
-            const float4* np = reinterpret_cast<const float4*>(S.nodes + code);
-            const float4 a = np[0], b = np[1], c = np[2];
-            const int4 k = reinterpret_cast<const int4*>(np)[3];
-#endif
             const f3 inv = t.inv, oi = t.oi;
             const float tx0 = fmaf(a.x, inv.x, oi.x), tx1 = fmaf(a.w, inv.x, oi.x);
             const float ty0 = fmaf(a.y, inv.y, oi.y), ty1 = fmaf(b.x, inv.y, oi.y);
@@ -556,7 +463,6 @@ ND void traverse_packet(const DScene& S, const Ray& r, float tmax, float& bestT,
                 // profiles/r05u_packet_pairs_ab.log)
                 for (uint32_t i = 0; i < count; ++i) {
                     if (COUNT) cnt.tris++;
-#if NART_PACKET_SLOAD
                     float4 tb, tc, dd, ta;
                     if (umaj) {  // every ray of the wave has this major axis: one scalar load
                         typedef float v4f __attribute__((ext_vector_type(4)));
@@ -573,9 +479,6 @@ ND void traverse_packet(const DScene& S, const Ray& r, float tmax, float& bestT,
                         dd = tpp[4 * i + 2];
                         ta = tpp[4 * i + 3];
                     }
-#else
-                    const float4 tb = tpp[4 * i], tc = tpp[4 * i + 1], dd = tpp[4 * i + 2], ta = tpp[4 * i + 3];
-#endif
                     f3 p0 = F3(tb.x - op.x, tb.y - op.y, tb.z - op.z);
                     f3 p1 = F3(tb.w - op.x, tc.x - op.y, tc.y - op.z);
                     f3 p2 = F3(tc.z - op.x, tc.w - op.y, dd.x - op.z);

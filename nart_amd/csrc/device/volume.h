@@ -181,9 +181,6 @@ ND bool maj_next(const DMedium& m, MajIter& it, float& sigma, float& t0, float& 
 #ifndef NART_VOL_WV
 #define NART_VOL_WV 4  // waves per SIMD of the throughput-bound launches (dispatch_volume)
 #endif
-#ifndef NART_VOL_PREFETCH
-#define NART_VOL_PREFETCH 1
-#endif
 template <bool COUNT, int WV>
 __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderArgs A) {
     // A.lds_nodes != 0: the density grid (that many floats) is staged in LDS
@@ -213,11 +210,9 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
     SlotSO so;
     const float2* smp = nullptr;
     float4* out = nullptr;
-#if NART_VOL_PREFETCH
     // the lane's next LatinSquare sample, loaded when the current one starts: a sample's first
     // iteration used to wait for its own load, and a wave waits whenever any lane starts a sample
     float2 nsm = make_float2(0.f, 0.f);
-#endif
     auto take = [&](uint32_t sl) {
         slot = sl;
         const uint32_t xy = A.slot_xy[sl];
@@ -229,9 +224,7 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
         out = A.Lout + so.first;
     };
     take(slot);
-#if NART_VOL_PREFETCH
     nsm = smp[0];
-#endif
     const DMedium& m = S.medium;
     const f3 beta = F3(1.f, 1.f, 1.f);
     enum { P_SAMPLE, P_RAY, P_MAJ, P_COLL, P_ESC, P_SCAT };
@@ -274,12 +267,8 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
         }
         if (ph == P_SAMPLE) {
             if (s >= A.spp) break;
-#if NART_VOL_PREFETCH
             const float2 sm = nsm;
             nsm = smp[(size_t)(s + 1u < A.spp ? s + 1u : s) * so.stride];
-#else
-            const float2 sm = smp[(size_t)s * so.stride];
-#endif
             const Ray r = cast_ray(S, F2(sm.x, sm.y), A.W, A.H, px, py);
             o = r.o;
             d = r.d;

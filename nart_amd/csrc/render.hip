@@ -131,6 +131,16 @@ int fail(nart_ctx* c, int code, const std::string& m) {
         }                                                                                        \
     } while (0)
 
+// Run-time switches, all read here.  Fallbacks a deployment can need: NART_BATCH_BYTES (per-batch
+// memory budget), NART_BVH_BUILD=device, NART_GATHER=rccl|copy.  The others are test hooks that
+// force one scheduling or kernel path of an otherwise automatic choice so that the GPU parity suite
+// covers it (tests/test_gpu_*.py; DESIGN.md section 2 lists them); none changes an image.
+const char* env_opt(const char* name) { return std::getenv(name); }
+double env_num(const char* name, double def) {
+    const char* e = env_opt(name);
+    return e && *e ? std::atof(e) : def;
+}
+
 template <typename T>
 int upload(nart_ctx* ctx, void*& dst, const T* src, size_t count) {
     size_t bytes = sizeof(T) * (count ? count : 1);
@@ -406,7 +416,7 @@ size_t batch_slot_limit(const nart_ctx* ctx, uint32_t spp) {
     } else {
         (void)hipGetLastError();
     }
-    if (const char* e = std::getenv("NART_BATCH_BYTES")) budget = (size_t)std::strtoull(e, nullptr, 10);
+    if (const char* e = env_opt("NART_BATCH_BYTES")) budget = (size_t)std::strtoull(e, nullptr, 10);
     size_t per = 8 + (size_t)spp * (sizeof(float2) + sizeof(float4) + sizeof(uint32_t));
     size_t n = budget / per;
     return n < 256 ? 256 : n;
@@ -500,17 +510,13 @@ uint32_t render_lds_nodes(const nart_ctx* ctx, size_t fixed = 0, uint32_t blocks
     const size_t budget = (size_t)160 * 1024 * blocks_of_256 / NART_RENDER_WAVES;
     size_t n = budget > stack ? (budget - stack) / sizeof(BVHNode) : 0;
     while (n && node_lds_bytes((uint32_t)n) > budget - stack) --n;  // NART_NODE_PAD padding
-    if (const char* e = std::getenv("NART_LDS_NODES")) n = (size_t)std::strtoul(e, nullptr, 10);
     return (uint32_t)std::min<size_t>(n, ctx->num_nodes);
 }
 
 // The ray-queue kernel's fixed LDS (stack + outboxes + results + id rings) fits one block per CU
 // (stack_depth <= 24 at 512 lanes).  NART_RQ_LDS_LIMIT lowers the budget (tests of the fallback).
 bool rq_fits(const nart_ctx* ctx) {
-    const size_t limit = std::getenv("NART_RQ_LDS_LIMIT")
-                                    ? std::min<size_t>(std::strtoull(std::getenv("NART_RQ_LDS_LIMIT"), nullptr, 10),
-                                                       (size_t)160 * 1024)
-                                    : (size_t)160 * 1024;
+    const size_t limit = (size_t)std::min(env_num("NART_RQ_LDS_LIMIT", 160.0 * 1024), 160.0 * 1024);
     return rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK) <= limit;
 }
 
@@ -655,10 +661,9 @@ __global__ void k_iota(uint32_t* v, uint32_t n) {
 #ifndef NART_RQ_GROUP_LANES
 #define NART_RQ_GROUP_LANES 2
 #endif
-int queue_mode() {
-    const char* e = std::getenv("NART_QUEUE");
-    return e ? std::max(0, std::min(2, std::atoi(e))) : 2;
-}
+// pixel work queue: 2 = cost probe + priority queue / wave-group refill (the schedule; 0, no
+// queue, and 1, refill in slot order, were A/B forms)
+constexpr int queue_mode() { return 2; }
 
 int sort_groups_by_cost(nart_ctx* ctx, uint32_t n, uint32_t* out, hipStream_t st) {
     const uint32_t ng = (n + 63) / 64;
@@ -711,8 +716,9 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
     ctx->fm_used = rq ? FM : FT_ALL;
     if (rq && FM != FT_ALL) ctx->sched |= NART_SCHED_SPECIALIZED;
     if (rq && WV == 3) ctx->sched |= NART_SCHED_LEAN;
-    // camera rays first, coherently (k_primary); NART_PRIMARY=0 leaves them to the path kernel
-    const bool primary = !std::getenv("NART_PRIMARY") || std::atoi(std::getenv("NART_PRIMARY")) != 0;
+    // camera rays first, coherently (k_primary; leaving them to the path kernel measured C3 470 vs
+    // 407 ms per frame, profiles/r02h_env_ab.log)
+    const bool primary = true;
 
     // rounds of resident waves from which a launch counts as throughput-bound: ray-queue quorum 8
     // (else 0), no priority lanes or speculative pairs
@@ -727,8 +733,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
         // camera rays as wave packets (path.h traverse_packet; C3 -1.7 ms, C4 -31 ms per frame,
         // profiles/r04_primary_packet_ab.log); NART_PRIMARY_PACKET=0 (read per call): one ray per lane
         RenderArgs pa = a;
-        const char* pp = std::getenv("NART_PRIMARY_PACKET");
-        pa.packet = pp ? (uint32_t)(std::atoi(pp) != 0) : 1u;
+        pa.packet = env_num("NART_PRIMARY_PACKET", 1.0) != 0.0 ? 1u : 0u;
         hipLaunchKernelGGL((k_primary<COUNT, ENV, FM>), dim3((a.n_slots + 255) / 256), dim3(256),
                            (size_t)ctx->stack_depth * 256 * 8, st, ctx->scene, pa, ctx->d_prim);
         HIPCHK(hipGetLastError());
@@ -759,12 +764,11 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
             // traversal-phase quorum: 8 on throughput-bound launches; 0 (every queued ray resolved
             // before the path phase) on small shards, whose costliest pixels' chains set the time
             // (1/8 C3 shard: 100.5 -> 96.0 ms)
-            const int rqq = std::getenv("NART_RQ_QUORUM") ? std::atoi(std::getenv("NART_RQ_QUORUM")) : -1;
             RenderArgs r2 = args;
             r2.lds_nodes = brq.lds_nodes;
             r2.prim = brq.prim;
             r2.stack_lds = skd;
-            r2.rq_quorum = rqq >= 0 ? (uint32_t)rqq : (R >= q_rounds ? 8u : 0u);
+            r2.rq_quorum = R >= q_rounds ? 8u : 0u;
             const uint32_t per = RQB / 256;  // launches are counted in blocks of 256
             const uint32_t grid = (nblocks + per - 1) / per;
             const size_t threads = (size_t)grid * RQB;
@@ -802,7 +806,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
             // costly pixels per first-round wave: few when the shard is small (their serial chains
             // bound the frame), all 64 (packed, launched first) when there are many rounds
             // the costly pixels on one wave per SIMD (NART_RQ_HALF=0: dealt over every wave; see below)
-            const bool half_want = rq && !(std::getenv("NART_RQ_HALF") && std::atoi(std::getenv("NART_RQ_HALF")) == 0);
+            const bool half_want = rq && env_num("NART_RQ_HALF", 1.0) != 0.0;
             // measured on C3 shards of 1/2, 1/4, 1/8 of the frame; with half_want 12 (2 x 12 on each
             // priority wave): C3 1/8 shard mean of the 8 ranks 4/6/8/12/14/16: 95.2/88.8/81.4/80.9/81.3/81.6 ms
             uint32_t k = R >= 3.0 ? 32u : (half_want ? 12u : 8u);
@@ -810,14 +814,13 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
             // rounds: 241 -> 235 ms; C4 batches, ~9 rounds: 1385 -> 1566 Msamples/s).  Below that a
             // wave of costly groups outlasts the rest (1/4 shard, 4 rounds: 146 -> 211 ms), and
             // the probe-ordered pixel queue with priority lanes stays
-            const double g_rounds =
-                std::getenv("NART_RQ_GROUP_MIN_ROUNDS") ? std::atof(std::getenv("NART_RQ_GROUP_MIN_ROUNDS")) : 6.0;
-            if (R >= (rq ? g_rounds : 12.0) && mode == 2 && !std::getenv("NART_QUEUE_K")) {
+            const double g_rounds = 6.0;
+            if (R >= (rq ? g_rounds : 12.0) && mode == 2 && !env_opt("NART_QUEUE_K")) {
                 // many rounds: the slot order (costly waves interleaved with cheap ones in time)
                 // measured faster than any reordering; no probe.  The ray-queue kernel runs it on
                 // a persistent grid whose waves take wave-sized slot groups in that order
-                // (NART_RQ_GROUPS=0: one wave per group, blocks retiring as a whole)
-                const bool groups = rq && (!std::getenv("NART_RQ_GROUPS") || std::atoi(std::getenv("NART_RQ_GROUPS")) != 0);
+                // (one wave per group, blocks retiring as a whole: 422 vs 407 ms, profiles/r02h_env_ab.log)
+                const bool groups = rq;
                 if (groups) {
                     int per_cu_rq = 0;
                     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_rq, (const void*)kern_rq, RQB,
@@ -830,7 +833,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
                     // glass) taken last left a tail: at 90 % of the C3 launch only 25 of 2,048
                     // waves were still running (WAVEPROF timeline).  C3 frame 445 -> 407 ms
                     // (probe included; order 1: 408, top 20 / 35 %: 408 / 408 ms)
-                    const int order = std::getenv("NART_RQ_ORDER") ? std::atoi(std::getenv("NART_RQ_ORDER")) : 2;
+                    const int order = (int)env_num("NART_RQ_ORDER", 2.0);
                     ctx->sched |= NART_SCHED_WAVE_GROUPS;
                     if (order == 1 || order == 2) {
                         // cost probe: the first sample of NART_PROBE_SUB (default 8) evenly spaced
@@ -842,10 +845,8 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
                         // sets the tail (C4 1/8 shards, 8 rounds: worst rank 488-496 ms probing every
                         // pixel, 552-556 ms sampled; profiles/r05ah_c4_probe_ab.log)
                         const uint32_t ng = (n + 63) / 64;
-                        const double sub_rounds =
-                            std::getenv("NART_PROBE_SUB_ROUNDS") ? std::atof(std::getenv("NART_PROBE_SUB_ROUNDS")) : 12.0;
-                        uint32_t sub = std::getenv("NART_PROBE_SUB") ? (uint32_t)std::atoi(std::getenv("NART_PROBE_SUB"))
-                                                                     : (R >= sub_rounds ? 8u : 64u);
+                        const double sub_rounds = 12.0;
+                        uint32_t sub = (uint32_t)env_num("NART_PROBE_SUB", R >= sub_rounds ? 8.0 : 64.0);
                         if (sub != 1u && sub != 2u && sub != 4u && sub != 8u && sub != 16u && sub != 32u) sub = 64u;
                         RenderArgs pb = b;
                         pb.spp = 1;
@@ -863,7 +864,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
                         if (order == 1) {
                             b.gorder = ctx->d_vals[1];
                         } else {
-                            const double f = std::getenv("NART_RQ_TOPF") ? std::atof(std::getenv("NART_RQ_TOPF")) : 10.0;
+                            const double f = env_num("NART_RQ_TOPF", 10.0);
                             const uint32_t E = (uint32_t)std::min<double>(ng, std::max(0.0, f) * 0.01 * ng);
                             hipLaunchKernelGGL(k_group_class, gg, block, 0, st, ctx->d_vals[1], ng, E, ctx->d_keys[0],
                                                ctx->d_vals[0]);
@@ -878,7 +879,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
                 }
                 return launch(blocks, b);
             }
-            if (const char* e = std::getenv("NART_QUEUE_K")) k = (uint32_t)std::max(1, std::min(64, std::atoi(e)));
+            if (env_opt("NART_QUEUE_K")) k = (uint32_t)std::max(1.0, std::min(64.0, env_num("NART_QUEUE_K", 8.0)));
             const bool refill = k < 64u || mode == 1;
             if (mode == 1) {
                 hipLaunchKernelGGL(k_iota, eg, block, 0, st, ctx->d_queue, n);
@@ -907,17 +908,16 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
                 // resident waves), whose time is their costliest pixels' chains: on throughput-bound
                 // launches the priority breaks and the speculative duplicates cost throughput
                 // (1/2 C3 shard 238 -> 249 ms, C4 batches 3175 -> 3381 ms with them on)
-                const int prio_env = std::getenv("NART_RQ_PRIO") ? std::atoi(std::getenv("NART_RQ_PRIO")) : 1;
+                const int prio_env = (int)env_num("NART_RQ_PRIO", 1.0);
                 const bool prio_on = prio_env == 2 || (prio_env == 1 && R < q_rounds);
                 // NART_RQ_PAIRS: lanes per costly pixel (0 off; 1 or 2 pairs; 4 groups of four)
-                const int pe = std::getenv("NART_RQ_PAIRS") ? std::atoi(std::getenv("NART_RQ_PAIRS")) : NART_RQ_GROUP_LANES;
+                const int pe = (int)env_num("NART_RQ_PAIRS", NART_RQ_GROUP_LANES);
                 const uint32_t Q = pe <= 0 ? 0u : (pe >= 4 ? 4u : 2u);
                 // (the lean build has no priority lanes: it runs only where prio_on is false anyway)
                 const uint32_t pbit = (rq && prio_on && WV != 3) ? RQ_PRIO_BIT : 0u;
                 const uint32_t pairs = (pbit && Q && Q * k <= 64u) ? Q : 0u;
                 // NART_RQ_QUAD (A/B): each first-round wave's costliest pixel gets four lanes
-                const bool quad = pbit && pairs == 2u && 2u * k + 2u <= 64u && std::getenv("NART_RQ_QUAD") &&
-                                  std::atoi(std::getenv("NART_RQ_QUAD")) != 0;
+                const bool quad = pbit && pairs == 2u && 2u * k + 2u <= 64u && env_num("NART_RQ_QUAD", 0.0) != 0.0;
                 const uint32_t qlen = n + (pairs ? (pairs - 1u) * k * W : 0u) + (quad ? 2u * W : 0u);
                 // Half waves (default): the costly pixels on the first 4 waves of each 8-wave block,
                 // 2k each -- one such wave per SIMD -- and those waves at a raised issue priority
@@ -928,8 +928,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
                 const bool half = pbit && half_want && (W % 8u) == 0u && 2u * (pairs ? pairs : 1u) * k <= 64u;
                 hipLaunchKernelGGL(k_build_queue, dim3((qlen + 255) / 256), block, 0, st, ctx->d_vals[1], ctx->d_vals[0],
                                    n, W, k, pbit, pairs, half ? 1u : 0u, quad ? 1u : 0u, ctx->d_queue);
-                const char* spe = std::getenv("NART_RQ_SETPRIO");
-                b.rq_setprio = pbit ? (spe ? (uint32_t)std::max(0, std::atoi(spe)) : (half ? 1u : 0u)) : 0u;
+                b.rq_setprio = pbit ? (uint32_t)std::max(0.0, env_num("NART_RQ_SETPRIO", half ? 1.0 : 0.0)) : 0u;
                 if (half) ctx->sched |= NART_SCHED_HALF_WAVES;
                 b.rq_prio = pbit ? 1u : 0u;
                 b.rq_pairs = pairs;
@@ -978,8 +977,8 @@ constexpr uint32_t FM_ENVTEX = FT_LAMBERT | FT_PLASTIC | FT_ENV | FT_TEX | FT_NM
 // nodes; 7 / 8 / 10 levels measured 241 / 241 / 245 ms per frame, +-7 ms run to run
 // (profiles/r06e_lean_stack_ab.log).  NART_LEAN_STACK (tests) forces a depth.
 uint32_t lean_stack(const nart_ctx* ctx) {
-    const char* e = std::getenv("NART_LEAN_STACK");
-    if (e) return std::max<uint32_t>(1u, std::min<uint32_t>(ctx->stack_depth, (uint32_t)std::atoi(e)));
+    if (env_opt("NART_LEAN_STACK"))
+        return std::max<uint32_t>(1u, std::min<uint32_t>(ctx->stack_depth, (uint32_t)env_num("NART_LEAN_STACK", 1.0)));
     const size_t nodes = std::min<size_t>(ctx->num_nodes, 320) * sizeof(BVHNode);
     uint32_t k = ctx->stack_depth;
     while (k > 4 && rq_lds_bytes(k, 768) + nodes > (size_t)160 * 1024) --k;
@@ -1018,7 +1017,10 @@ int dispatch_megakernel(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             if (lean_fits(ctx, a)) return launch_render<false, false, false, FM_GLASS, 3>(ctx, a, st);
             return launch_render<false, false, false, FM_GLASS>(ctx, a, st);
         }
-        if (ctx->has_env && covers(FM_ENVTEX)) return launch_render<false, false, true, FM_ENVTEX>(ctx, a, st);
+        if (ctx->has_env && covers(FM_ENVTEX)) {
+            if (lean_fits(ctx, a)) return launch_render<false, false, true, FM_ENVTEX, 3>(ctx, a, st);
+            return launch_render<false, false, true, FM_ENVTEX>(ctx, a, st);
+        }
     }
     return ctx->has_env ? launch_render_maxl<true>(ctx, a, st) : launch_render_maxl<false>(ctx, a, st);
 }
@@ -1031,10 +1033,9 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     const dim3 block(256);
     const uint32_t blocks = (a.n_slots + 255) / 256;
     RenderArgs b = a;
-    // small density grids (C5: 2x2x2) are read from LDS (NART_VOL_LDS=0: from global memory)
-    const bool vol_lds = !(std::getenv("NART_VOL_LDS") && std::getenv("NART_VOL_LDS")[0] == '0');
+    // small density grids (C5: 2x2x2) are read from LDS (1 % faster than L1-hitting global loads)
     const uint32_t nd = ctx->scene.medium.present ? ctx->scene.medium.rx * ctx->scene.medium.ry * ctx->scene.medium.rz : 0;
-    b.lds_nodes = (vol_lds && nd <= 4096u) ? nd : 0u;
+    b.lds_nodes = nd <= 4096u ? nd : 0u;
     const size_t dl = (size_t)b.lds_nodes * sizeof(float);
     // occupancy: launches of >= 8 rounds of resident waves use the 4-waves-per-SIMD build (C5 frame,
     // 10.5 rounds: 134 -> 122 ms); smaller ones keep the unconstrained build, whose lanes' serial
@@ -1044,7 +1045,7 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_render_volume_sm<false, 1>, 256, dl));
     const uint32_t resident = (uint32_t)std::max(1, cus * std::max(per_cu, 1));
-    const double w4_rounds = std::getenv("NART_VOL_W4_ROUNDS") ? std::atof(std::getenv("NART_VOL_W4_ROUNDS")) : 8.0;
+    const double w4_rounds = 8.0;
     const bool w4 = (double)blocks / (double)resident >= w4_rounds;
     uint32_t grid = blocks;
     if (queue_mode() == 2) {
@@ -1069,11 +1070,8 @@ int dispatch_volume(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
             // C5 1/8 shard 73.7 -> 65.3 ms; on larger shards (2+ rounds) the mostly idle sparse
             // waves hold slots the other groups need (1/2 shard 78 -> 127 ms), and 1-8 pixels per
             // wave measured worse (profiles/r04h_c5_sparse.log).  Only the order of work changes.
-            const char* se = std::getenv("NART_VOL_SPARSE");
-            const char* fe = std::getenv("NART_VOL_SPARSE_F");
-            const char* re = std::getenv("NART_VOL_SPARSE_ROUNDS");
-            const uint32_t S = se ? std::max(1u, std::min(64u, (uint32_t)std::atoi(se))) : 16u;
-            const double f = fe ? std::atof(fe) : 4.0, max_rounds = re ? std::atof(re) : 2.0;
+            const uint32_t S = (uint32_t)std::max(1.0, std::min(64.0, env_num("NART_VOL_SPARSE", 16.0)));
+            const double f = env_num("NART_VOL_SPARSE_F", 4.0), max_rounds = env_num("NART_VOL_SPARSE_ROUNDS", 2.0);
             if (S < 64u && (64u % S) == 0u && (double)blocks / (double)resident < max_rounds) {
                 const uint32_t ng = (n + 63) / 64;
                 std::vector<uint32_t> keys(ng);
@@ -1196,7 +1194,6 @@ bool splat_lut(const float thr[65], const float table[64], std::vector<float4>& 
 // slot once there are >= 64 slots), the global-memory variant beyond.
 int launch_latin(nart_ctx* ctx, const RenderArgs& ra, hipStream_t st) {
     // three-kernel form (k_latin_draws / _perm / _emit) when its scratch fits in Lout
-    const int latin_env = std::getenv("NART_LATIN") ? std::atoi(std::getenv("NART_LATIN")) : -1;
     const uint32_t groups = (ra.n_slots + 63) / 64;
     LatinScratch ls;
     ls.n2 = (ra.spp + 1) / 2;
@@ -1206,7 +1203,7 @@ int launch_latin(nart_ctx* ctx, const RenderArgs& ra, hipStream_t st) {
     const size_t stw = (size_t)((ra.n_slots + LATIN_EMIT_SLOTS - 1) / LATIN_EMIT_SLOTS) * LATIN_EMIT_SLOTS * ra.spp +
                        LATIN_ST_PAD;
     const bool three = ra.spp >= 2 && ra.spp <= 1024 && (4 * words + stw) * 4 <= ctx->cap_samples * sizeof(float4) &&
-                       (latin_env == 3 || (latin_env < 0 && ra.spp > 64));  // C3 (256 spp): 6.7 -> 4.6 ms
+                       ra.spp > 64;  // C3 (256 spp): 6.7 -> 4.6 ms
     if (three) {
         uint32_t* base = reinterpret_cast<uint32_t*>(ra.Lout);
         ls.cx = base;
@@ -1235,50 +1232,6 @@ int launch_latin(nart_ctx* ctx, const RenderArgs& ra, hipStream_t st) {
     return NART_OK;
 }
 
-#ifdef NART_WAVEPROF
-// k_render_rq chain records (NART_WAVEPROF builds, NART_CHAIN_REPORT set; development profile)
-int chain_report(nart_ctx* ctx, const std::vector<uint32_t>& xy) {
-    // k_render_rq chain records (first pixel of each lane): the last-finishing chains'
-    // critical-path split, shader cycles: own rays outstanding (queued or traced) / own rays
-    // resolved while the traversal phase serves others / path phases in which it shaded
-    // or started samples / path phases of other lanes / lane idle in traversal
-    std::vector<unsigned long long> r(8 * (size_t)RQ_CHAIN_MAX);
-    HIPCHK(hipMemcpy(r.data(), ctx->d_counters + RQ_CHAIN_OFF, r.size() * 8, hipMemcpyDeviceToHost));
-    std::vector<std::pair<unsigned long long, uint32_t>> fin;
-    double sum[6] = {0, 0, 0, 0, 0, 0}, psum[6] = {0, 0, 0, 0, 0, 0};
-    uint32_t np = 0;
-    for (uint32_t i = 0; i < RQ_CHAIN_MAX; ++i)
-        if (r[8 * i] >> 34) {
-            fin.push_back({r[8 * i + 1], i});
-            const bool pr = (r[8 * i] >> 32) & 1u;
-            for (int k = 0; k < 6; ++k) {
-                const double v = (double)r[8 * i + 2 + k];
-                sum[k] += v;
-                if (pr) psum[k] += v;
-            }
-            np += pr ? 1u : 0u;
-        }
-    std::sort(fin.begin(), fin.end());
-    const double n = (double)std::max<size_t>(1, fin.size());
-    fprintf(stderr, "CHAIN records %zu (priority %u) mean cycles: own_rays %.0f wait_others %.0f shade %.0f "
-                    "other_path %.0f idle %.0f total %.0f\n", fin.size(), np, sum[0] / n, sum[1] / n, sum[2] / n,
-            sum[3] / n, sum[4] / n, sum[5] / n);
-    if (np)
-        fprintf(stderr, "CHAIN priority mean cycles: own_rays %.0f wait_others %.0f shade %.0f other_path %.0f "
-                        "idle %.0f total %.0f\n", psum[0] / np, psum[1] / np, psum[2] / np, psum[3] / np,
-                psum[4] / np, psum[5] / np);
-    for (size_t k = 0; k < 8 && k < fin.size(); ++k) {
-        const uint32_t i = fin[fin.size() - 1 - k].second;
-        const unsigned long long* q = &r[8 * (size_t)i];
-        const uint32_t sl = (uint32_t)(q[0] & 0xFFFFFFFFu);
-        fprintf(stderr, "CHAIN last#%zu lane %u slot %u px (%u,%u) prio %d pair %d finish %.3f ms cycles: own_rays "
-                        "%llu wait_others %llu shade %llu other_path %llu idle %llu total %llu\n",
-                k, i, sl, sl < xy.size() ? xy[sl] & 0xFFFFu : 0u, sl < xy.size() ? xy[sl] >> 16 : 0u,
-                (int)((q[0] >> 32) & 1u), (int)((q[0] >> 33) & 1u), q[1] * 1e-5, q[2], q[3], q[4], q[5], q[6], q[7]);
-    }
-    return NART_OK;
-}
-#endif
 
 // Render a bucket list into device tiles (list order).  Shared by all entry points.
 int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* ids, uint32_t n, float* d_tiles,
@@ -1299,16 +1252,14 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
     HIPCHK(hipMemcpy(ctx->d_table, table, sizeof(table), hipMemcpyHostToDevice));
     std::vector<float4> lut;
     uint32_t lut_b0 = 0;
-    const bool lut_env = !(std::getenv("NART_SPLAT_LUT") && std::getenv("NART_SPLAT_LUT")[0] == '0');
-    const bool lut_ok = lut_env && thr_ok && splat_lut(table + 64, table, lut, lut_b0);
+    const bool lut_ok = thr_ok && splat_lut(table + 64, table, lut, lut_b0);
     // skewed-time splat (k_splat_skew, pixel-major samples) where its preconditions hold, else
     // k_splat_col4 / k_splat over the sample-major layout
     // It runs one lane per tile column for ~W*B steps, so its time is one wave's latency once the
     // launch has fewer than ~2 waves per SIMD: small shards keep k_splat_col4 (C5 1/8 shard:
-    // 54 ms skewed vs 23 ms col4; whole frame 72 vs 113 ms).  NART_SKEW_MIN_WAVES: waves per SIMD.
+    // 54 ms skewed vs 23 ms col4; whole frame 72 vs 113 ms).  skew_min: waves per SIMD.
     const uint32_t B = p->bucket_size, tile = B + 2 * g.filter_bounds;
-    const double skew_min =
-        std::getenv("NART_SKEW_MIN_WAVES") ? std::atof(std::getenv("NART_SKEW_MIN_WAVES")) : 2.0;
+    const double skew_min = 2.0;
     int n_cus = 0;
     HIPCHK(hipDeviceGetAttribute(&n_cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
     const double skew_waves = tile <= 64 ? (double)((n + 64 / tile - 1) / (64 / tile)) : 0.0;
@@ -1323,12 +1274,12 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
     const double skew_from = p->integrator == NART_INTEGRATOR_VOLUME ? 0.5 * skew_min : skew_min;
     // Below that, k_splat_rows (mode 5: W lanes per tile column, five times k_splat_skew's
     // parallelism, each sample still fetched once per bucket) unless NART_SPLAT_SMALL=col4
-    const char* ss = std::getenv("NART_SPLAT_SMALL");
+    const char* ss = env_opt("NART_SPLAT_SMALL");
     const int small_mode = ss && std::strcmp(ss, "col4") == 0 ? 3 : 5;
     const int splat_mode =
         ctx->splat_mode >= 0 ? ctx->splat_mode : (skew_waves >= skew_from * 4.0 * n_cus ? 4 : small_mode);
     // NART_SKEW_BANDS (read per call): 1 or 2 forces the band count
-    const char* be = std::getenv("NART_SKEW_BANDS");
+    const char* be = env_opt("NART_SKEW_BANDS");
     const uint32_t skew_bands = be && std::atoi(be) > 0 ? (std::atoi(be) >= 2 ? 2u : 1u)
                                                           : (skew_waves >= skew_min * 4.0 * n_cus ? 1u : 2u);
     // skew: a pixel-major sample layout for k_splat_skew (mode 4) or k_splat_rows (mode 5)
@@ -1339,17 +1290,9 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         if (!ctx->d_lut) HIPCHK(hipMalloc(&ctx->d_lut, SPLAT_LUT_MAX * sizeof(float4)));
         HIPCHK(hipMemcpy(ctx->d_lut, lut.data(), lut.size() * sizeof(float4), hipMemcpyHostToDevice));
     }
-#ifdef NART_WAVEPROF
-    // + per-wave and per-slot records, + k_render_rq chain records (development profile)
-    const size_t n_cnt = RQ_CHAIN_OFF + 8 * (size_t)RQ_CHAIN_MAX;
-#else
     const size_t n_cnt = 24;
-#endif
     if (!ctx->d_counters) HIPCHK(hipMalloc(&ctx->d_counters, n_cnt * sizeof(unsigned long long)));
     if (ctx->counters) HIPCHK(hipMemsetAsync(ctx->d_counters, 0, n_cnt * sizeof(unsigned long long), st));
-#ifdef NART_WAVEPROF
-    else HIPCHK(hipMemsetAsync(ctx->d_counters + RQ_CHAIN_OFF, 0, 8 * (size_t)RQ_CHAIN_MAX * 8, st));
-#endif
     if (!ctx->events) {
         for (auto& e : ctx->ev) HIPCHK(hipEventCreate(&e));
         ctx->events = true;
@@ -1497,9 +1440,6 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
         splat_ms += ms;
         HIPCHK(hipEventElapsedTime(&ms, ctx->ev[3], ctx->ev[0]));
         latin_ms += ms;
-#ifdef NART_WAVEPROF
-        if (std::getenv("NART_CHAIN_REPORT") && (rc = chain_report(ctx, xy))) return rc;
-#endif
         ++launches;
         b0 = b1;
     }
@@ -1522,79 +1462,6 @@ int render_buckets(nart_ctx* ctx, const nart_render_params* p, const uint32_t* i
             stats->bounces += c[4];
             stats->octree_checks += c[5];
             stats->octree_replays += c[6];
-#ifdef NART_WAVEPROF
-            unsigned long long w[24];
-            HIPCHK(hipMemcpy(w, ctx->d_counters, sizeof(w), hipMemcpyDeviceToHost));
-            {
-                const uint32_t nw = (uint32_t)std::min<size_t>((xy.size() + 63) / 64, 70000);
-                std::vector<unsigned long long> pw(8 * (size_t)nw);
-                HIPCHK(hipMemcpy(pw.data(), ctx->d_counters + 24, pw.size() * 8, hipMemcpyDeviceToHost));
-                std::vector<std::pair<unsigned long long, uint32_t>> cy;
-                for (uint32_t i = 0; i < nw; ++i) cy.push_back({pw[8 * i], i});
-                std::sort(cy.begin(), cy.end());
-                auto q = [&](double f) { return cy[(size_t)(f * (cy.size() - 1))].first; };
-                unsigned long long rp = 0, rp_top = 0;
-                for (uint32_t i = 0; i < nw; ++i) rp += pw[4 * i + 1];
-                for (size_t k = 0; k < cy.size() / 100; ++k) rp_top += pw[4 * cy[cy.size() - 1 - k].second + 1];
-                {
-                    const uint32_t m = cy[cy.size() / 2].second;
-                    fprintf(stderr, "WAVEPROF median wave cycles %llu trav %llu iterations %llu node-iters %llu/%llu tri-iters %llu/%llu\n",
-                            pw[8 * m], pw[8 * m + 1], pw[8 * m + 2], pw[8 * m + 4], pw[8 * m + 5], pw[8 * m + 6], pw[8 * m + 7]);
-                }
-                fprintf(stderr, "WAVEPROF waves %u cycles p10 %llu p50 %llu p90 %llu p99 %llu max %llu\n", nw, q(0.1), q(0.5),
-                        q(0.9), q(0.99), q(1.0));
-                for (size_t k = 0; k < 6 && k < cy.size(); ++k) {
-                    const uint32_t i = cy[cy.size() - 1 - k].second;
-                    const uint32_t s0 = (uint32_t)pw[8 * i + 3];
-                    fprintf(stderr, "WAVEPROF top wave %u cycles %llu trav-cycles %llu iterations %llu node-iters %llu/%llu tri-iters %llu/%llu px (%u,%u)\n", i, pw[8 * i],
-                            pw[8 * i + 1], pw[8 * i + 2], pw[8 * i + 4], pw[8 * i + 5], pw[8 * i + 6], pw[8 * i + 7], s0 < xy.size() ? xy[s0] & 0xFFFF : 0, s0 < xy.size() ? xy[s0] >> 16 : 0);
-                }
-            }
-            {
-                // ray-queue kernel wave timeline (s_memrealtime, 100 MHz): waves still running at
-                // fractions of the launch span
-                const uint32_t nw = (uint32_t)std::min<size_t>((xy.size() + 63) / 64, 70000);
-                std::vector<unsigned long long> pw(2 * (size_t)nw);
-                HIPCHK(hipMemcpy(pw.data(), ctx->d_counters + 24 + 8 * 70000 + 4200000 - 2 * 70000, pw.size() * 8,
-                                 hipMemcpyDeviceToHost));
-                unsigned long long t0 = ~0ull, t1 = 0;
-                uint32_t nv = 0;
-                for (uint32_t i = 0; i < nw; ++i)
-                    if (pw[2 * i + 1]) {
-                        t0 = std::min(t0, pw[2 * i]);
-                        t1 = std::max(t1, pw[2 * i + 1]);
-                        ++nv;
-                    }
-                if (nv) {
-                    fprintf(stderr, "WAVETL waves %u span %.2f ms; running at", nv, (t1 - t0) * 1e-5);
-                    for (double f : {0.1, 0.25, 0.4, 0.5, 0.6, 0.7, 0.8, 0.9, 0.95}) {
-                        const unsigned long long t = t0 + (unsigned long long)(f * (t1 - t0));
-                        uint32_t run = 0;
-                        for (uint32_t i = 0; i < nw; ++i)
-                            if (pw[2 * i + 1] && pw[2 * i] <= t && pw[2 * i + 1] > t) ++run;
-                        fprintf(stderr, " %.0f%%:%u", f * 100, run);
-                    }
-                    fprintf(stderr, "\n");
-                }
-            }
-            if (const char* dump = std::getenv("NART_WAVEPROF_DUMP")) {
-                std::vector<unsigned long long> ps(xy.size());
-                HIPCHK(hipMemcpy(ps.data(), ctx->d_counters + 24 + 8 * 70000, ps.size() * 8, hipMemcpyDeviceToHost));
-                if (FILE* f = fopen(dump, "wb")) {
-                    fwrite(xy.data(), 4, xy.size(), f);
-                    fwrite(ps.data(), 8, ps.size(), f);
-                    fclose(f);
-                }
-            }
-            {
-                unsigned long long sc[8];
-                HIPCHK(hipMemcpy(sc, ctx->d_counters + 24 + 8 * 69999, sizeof(sc), hipMemcpyDeviceToHost));
-                fprintf(stderr, "WAVEPROF rq path sections results+shading %llu refill %llu new_samples %llu id_lists %llu shadow nodes %llu tris %llu\n",
-                        sc[0], sc[1], sc[2], sc[3], sc[4], sc[5]);
-            }
-            fprintf(stderr, "WAVEPROF steps %llu/%llu nodes %llu/%llu tris %llu/%llu trav_cyc %llu total_cyc %llu shade %llu/%llu phases %llu path_cyc %llu\n",
-                    w[8], w[9], w[10], w[11], w[12], w[13], w[14], w[15], w[16], w[17], w[18], w[19]);
-#endif
         }
     }
     return NART_OK;
@@ -1723,11 +1590,11 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     if (!ctx) return NART_E_OOM;
     *out = nullptr;
     ctx->device = device_id;
-    if (const char* v = std::getenv("NART_VARIANT")) {
+    if (const char* v = env_opt("NART_VARIANT")) {
         const int var = std::atoi(v);
         if (var == 0 || var == 3) ctx->variant = var;
     }
-    if (const char* v = std::getenv("NART_SPLAT_MODE")) ctx->splat_mode = std::max(-1, std::min(5, std::atoi(v)));
+    if (const char* v = env_opt("NART_SPLAT_MODE")) ctx->splat_mode = std::max(-1, std::min(5, std::atoi(v)));
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device_id || device_id < 0) {
         delete ctx;
@@ -1771,7 +1638,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     if ((rc = upload(ctx, ctx->d_tris, blob->triangles, blob->num_triangles))) return bail(rc);
     // NART_BVH_BUILD=device: linear BVH built on the GPU (device/lbvh.h); default: binned SAH on
     // the host (host/bvh_build.cpp) -- same node / record format, same images
-    const char* bb = std::getenv("NART_BVH_BUILD");
+    const char* bb = env_opt("NART_BVH_BUILD");
     ctx->bvh_on_device = bb && std::string(bb) == "device";
     const auto tb0 = std::chrono::steady_clock::now();
     LbvhResult lb;
@@ -1914,11 +1781,11 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     S.oc_root = oct.root;
     S.oc_cap = (uint32_t)std::max<size_t>(oct.nodes.size(), 1);
     S.oc_pool = (uint32_t)std::max<size_t>(1, std::min<size_t>(512, (256ull << 20) / (64ull * 8ull * S.oc_cap)));
-    if (const char* v = std::getenv("NART_OC_POOL")) S.oc_pool = (uint32_t)std::max(1, std::atoi(v));
+    if (const char* v = env_opt("NART_OC_POOL")) S.oc_pool = (uint32_t)std::max(1, std::atoi(v));
     S.oc_scale = maxabs;
     S.oc_exact = 1;
     // NART_OCTREE_EXACT: 0 off (A/B timing only), 2 every query replays the octree search (tests)
-    if (const char* v = std::getenv("NART_OCTREE_EXACT")) S.oc_exact = std::max(0, std::min(2, std::atoi(v)));
+    if (const char* v = env_opt("NART_OCTREE_EXACT")) S.oc_exact = std::max(0, std::min(2, std::atoi(v)));
     if (hipMalloc(&ctx->d_oc_lock, sizeof(uint32_t) * S.oc_pool) != hipSuccess ||
         hipMemset(ctx->d_oc_lock, 0, sizeof(uint32_t) * S.oc_pool) != hipSuccess ||
         hipMalloc(&ctx->d_oc_heap, sizeof(unsigned long long) * 64 * S.oc_pool * S.oc_cap) != hipSuccess)
@@ -2138,16 +2005,9 @@ int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t
     if (rc) return rc;
     HIPCHK(hipMemcpy(ctx->d_slot_xy, xy.data(), (size_t)n * 4, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(k_slot_rows, dim3((n + 255) / 256), dim3(256), 0, 0, n, p->spp, ctx->d_slot_so);
-#ifdef NART_WAVEPROF
-    const size_t n_cnt = RQ_CHAIN_OFF + 8 * (size_t)RQ_CHAIN_MAX;  // as the bucket path (development profile)
-#else
     const size_t n_cnt = 24;
-#endif
     if (!ctx->d_counters) HIPCHK(hipMalloc(&ctx->d_counters, n_cnt * sizeof(unsigned long long)));
     if (ctx->counters) HIPCHK(hipMemset(ctx->d_counters, 0, n_cnt * sizeof(unsigned long long)));
-#ifdef NART_WAVEPROF
-    else HIPCHK(hipMemset(ctx->d_counters + RQ_CHAIN_OFF, 0, 8 * (size_t)RQ_CHAIN_MAX * 8));
-#endif
     RenderArgs ra;
     ra.slot_xy = ctx->d_slot_xy;
     ra.slot_so = ctx->d_slot_so;
@@ -2166,56 +2026,11 @@ int nart_hip_render_samples(nart_ctx* ctx, const nart_render_params* p, uint32_t
     ra.counters = ctx->d_counters;
     rc = launch_latin(ctx, ra, 0);
     if (rc) return rc;
-#ifdef NART_DEVPROBE
-    // development probe of the speculative pairs (tools/pair_latency.py; build with
-    // NART_HIP_DEFINES=-DNART_DEVPROBE): every pixel of the rect on two or four lanes
-    if (std::getenv("NART_SAMPLES_PAIRS") && std::atoi(std::getenv("NART_SAMPLES_PAIRS")) && ctx->variant == 0 &&
-        p->integrator == NART_INTEGRATOR_PATH && n <= 65536) {
-        if (ctx->has_env || p->bounces > 10) return fail(ctx, NART_E_UNSUPPORTED, "pairs probe: glass-like scenes only");
-        // the ray-queue kernel alone, camera rays included; no work queue refill
-        const uint32_t Q = std::atoi(std::getenv("NART_SAMPLES_PAIRS")) >= 4 ? 4u : 2u;  // lanes per pixel
-        rc = ensure_queue(ctx, Q * n);
-        if (rc) return rc;
-        std::vector<uint32_t> q(Q * n);
-        for (uint32_t i = 0; i < Q * n; ++i) q[i] = (i / Q) | RQ_PRIO_BIT | RQ_PAIR_BIT;
-        HIPCHK(hipMemcpy(ctx->d_queue, q.data(), q.size() * 4, hipMemcpyHostToDevice));
-        RenderArgs r2 = ra;
-        r2.queue = ctx->d_queue;
-        r2.qlen = Q * n;
-        r2.rq_prio = 1;
-        r2.rq_pairs = Q;
-        r2.rq_quorum = 0;
-        r2.lds_nodes = render_lds_nodes(ctx, rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK), NART_RQ_BLOCK / 256);
-        const size_t lds_rq = rq_lds_bytes(ctx->stack_depth, NART_RQ_BLOCK) + node_lds_bytes(r2.lds_nodes);
-        static bool attr = false;
-        auto kern = k_render_rq<false, false, false>;
-        if (!attr) {
-            hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            attr = true;
-        }
-        hipLaunchKernelGGL(kern, dim3((Q * n + NART_RQ_BLOCK - 1) / NART_RQ_BLOCK), dim3(NART_RQ_BLOCK), lds_rq, 0,
-                           ctx->scene, r2);
-        HIPCHK(hipGetLastError());
-    } else
-#endif
     {
         rc = dispatch_render(ctx, ra, p->integrator, 0);
         if (rc) return rc;
     }
     HIPCHK(hipMemcpy(out, ctx->d_L, (size_t)n * p->spp * sizeof(float4), hipMemcpyDeviceToHost));
-#ifdef NART_WAVEPROF
-    if (std::getenv("NART_CHAIN_REPORT") && (rc = chain_report(ctx, xy))) return rc;
-    if (ctx->counters) {
-        unsigned long long c[24], sc[8];
-        HIPCHK(hipMemcpy(c, ctx->d_counters, sizeof(c), hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(sc, ctx->d_counters + 24 + 8 * 69999, sizeof(sc), hipMemcpyDeviceToHost));
-        fprintf(stderr, "WAVEPROF samples: ext %llu shadow %llu nodes %llu tris %llu bounces %llu\n", c[0], c[1], c[2], c[3], c[4]);
-        fprintf(stderr, "WAVEPROF rq path sections results+shading %llu refill %llu new_samples %llu id_lists %llu shadow nodes %llu tris %llu\n",
-                sc[0], sc[1], sc[2], sc[3], sc[4], sc[5]);
-        fprintf(stderr, "WAVEPROF steps %llu/%llu nodes %llu/%llu tris %llu/%llu trav_cyc %llu total_cyc %llu shade %llu/%llu phases %llu path_cyc %llu\n",
-                c[8], c[9], c[10], c[11], c[12], c[13], c[14], c[15], c[16], c[17], c[18], c[19]);
-    }
-#endif
     return NART_OK;
 }
 
@@ -2316,7 +2131,7 @@ int nart_hip_shard_buckets(uint32_t n_buckets_x, uint32_t n_buckets, uint32_t n_
 int nart_hip_create_multi(const nart_scene_blob* blob, const int* device_ids, int n_devices, nart_ctx** out) {
     if (!blob || !out || !device_ids || n_devices < 1 || n_devices > 64) return NART_E_INVALID;
     *out = nullptr;
-    const char* gm = std::getenv("NART_GATHER");
+    const char* gm = env_opt("NART_GATHER");
     const bool force_rccl = gm && std::string(gm) == "rccl";
     const bool force_copy = gm && std::string(gm) == "copy";
     if (n_devices == 1 && !force_rccl) return nart_hip_create(blob, device_ids[0], out);

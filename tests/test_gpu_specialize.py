@@ -94,9 +94,11 @@ def test_cornell_lean_build(gpu, cornell_scene):
     assert _same_bits(a, b)
 
 
-def test_c4_specialised(gpu, c4_scene):
-    a, b, feats, build, _ = _both(c4_scene, _params(c4_scene, 384, 216, 4))
+@pytest.mark.parametrize("w,h,spp,lean", [(384, 216, 4, False), (1280, 720, 2, True)], ids=["small", "lean"])
+def test_c4_specialised(gpu, c4_scene, w, h, spp, lean):
+    a, b, feats, build, sched = _both(c4_scene, _params(c4_scene, w, h, spp))
     assert feats == FM_ENVTEX and build == FM_ENVTEX, (hex(feats), hex(build))
+    assert ("lean" in sched) == lean, sched
     assert _same_bits(a, b)
 
 

@@ -24,6 +24,17 @@ def _key(name):
     return name.split("(")[0].replace("void ", "")
 
 
+def waves_per_simd(vgpr, lds=None):
+    """Resident waves per SIMD the kernel's registers (and LDS, 160 KiB per CU) allow: 512 VGPRs
+    per SIMD lane in 8-register granules, at most 8 waves."""
+    try:
+        v = int(vgpr)
+    except (TypeError, ValueError):
+        return None
+    v = max(8, (v + 7) // 8 * 8)
+    return min(8, 512 // v)
+
+
 def _rows(src, kind):
     path = os.path.join(src, kind, "run_counter_collection.csv")
     return list(csv.DictReader(open(path))) if os.path.exists(path) else []
@@ -75,6 +86,15 @@ def main(src, tag, config="1920x1080x256"):
             e["lane_utilization"] = top.get("SQ_THREAD_CYCLES_VALU", 0.0) / (64.0 * av) if av else None
             e["wait_any"] = top.get("SQ_WAIT_ANY", 0.0) / wc
             e["wait_inst_any"] = top.get("SQ_WAIT_INST_ANY", 0.0) / wc
+            # issue rate: a wave issues at most one instruction per quad-cycle (the SQ counters'
+            # unit), so (VALU + SALU issue quad-cycles) / wave quad-cycles is the wave's issue
+            # fraction; times the waves resident per SIMD it is the SIMD's issue-slot occupancy
+            if "SQ_ACTIVE_INST_SALU" in top:
+                iw = (av + top["SQ_ACTIVE_INST_SALU"]) / wc
+                wps = waves_per_simd(d["vgpr"], d.get("lds"))
+                e["issue_frac_wave"] = iw
+                e["waves_per_simd"] = wps
+                e["issue_frac"] = min(1.0, iw * wps) if wps else None
         out["kernels"][k] = e
 
     def timed(name, base):
@@ -100,6 +120,9 @@ def main(src, tag, config="1920x1080x256"):
             out["render_kernel"] = pr[0] + " + " + rq[0]
         out["lane_utilization"] = r.get("lane_utilization")
         out["valu_busy"] = r.get("valu_busy")
+        out["issue_frac"] = r.get("issue_frac")
+        out["issue_frac_wave"] = r.get("issue_frac_wave")
+        out["waves_per_simd"] = r.get("waves_per_simd")
     json.dump(out, open(os.path.join(prof, tag + "_pmc.json"), "w"), indent=1)
     # bench.py reads pmc_latest_<config>.json (and pmc_latest.json for the headline C3 config)
     json.dump(out, open(os.path.join(prof, "pmc_latest_%s.json" % config), "w"), indent=1)
