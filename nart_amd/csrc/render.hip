@@ -755,9 +755,17 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
     int cus = 0, per_cu = 0;
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 256, lds));
-    const uint32_t resident = (uint32_t)std::max(1, cus * std::max(per_cu, 1));
+    const uint32_t resident_k = (uint32_t)std::max(1, cus * std::max(per_cu, 1));
+    // rounds of resident waves (of k_render: the same figure for every build, so that the lean
+    // build's choice, lean_fits, and this launch's thresholds agree)
+    const double R = (double)a.n_slots / (64.0 * 4.0 * resident_k);
+    // resident blocks of 256 lanes of the kernel this launch runs: the ray-queue kernel holds one
+    // 512- or 768-lane block per CU, so its persistent grid and the waves the queue deals its
+    // first round over are its own (the lean build has 1.5x k_render's resident lanes)
+    int per_cu_rq = 0;
+    if (rq) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_rq, (const void*)kern_rq, RQB, lds_rq));
+    const uint32_t resident = rq ? (uint32_t)std::max(1, cus * std::max(per_cu_rq, 1)) * (RQB / 256) : resident_k;
     const uint32_t W = resident * 4;  // resident (persistent) waves
-    const double R = (double)a.n_slots / (64.0 * W);  // rounds of resident waves
     // the ray-queue kernel takes kern's place (its own LDS layout); the cost probe keeps k_render
     auto launch = [&](uint32_t nblocks, const RenderArgs& args) -> int {
         if (rq) {
@@ -822,9 +830,6 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
                 // (one wave per group, blocks retiring as a whole: 422 vs 407 ms, profiles/r02h_env_ab.log)
                 const bool groups = rq;
                 if (groups) {
-                    int per_cu_rq = 0;
-                    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_rq, (const void*)kern_rq, RQB,
-                                                                       lds_rq));
                     HIPCHK(hipMemsetAsync(ctx->d_qhead, 0, sizeof(uint32_t), st));
                     b.ghead = ctx->d_qhead;
                     // group order (NART_RQ_ORDER): 0 slot order; 1 costliest group first (cost
@@ -875,7 +880,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
                         }
                     }
                     // launches are counted in blocks of 256 threads
-                    blocks = std::min(blocks, (uint32_t)std::max(1, cus * std::max(per_cu_rq, 1)) * (RQB / 256));
+                    blocks = std::min(blocks, resident);
                 }
                 return launch(blocks, b);
             }
@@ -998,11 +1003,17 @@ double launch_rounds(nart_ctx* ctx, uint32_t n) {
     return (double)n / (64.0 * W);
 }
 
-// The lean three-waves-per-SIMD build (kernels.h WV = 3): throughput-bound launches whose ray-queue
-// LDS fits a 768-lane block (stack depth <= 10 with the top BVH nodes after it)
+// The lean three-waves-per-SIMD build (kernels.h WV = 3) for throughput-bound launches.  It raises
+// throughput (C3 whole frame, 16 rounds of resident waves: path kernels 276.6 -> ~241 ms; C4 4K
+// frame and its 1/8 shards, 8 rounds: 492 -> 456 ms) but each of its waves runs slower, which
+// lengthens the serial sample chains of a scene's costliest pixels.  Glass scenes' chains (caustic
+// paths behind the dielectric) set the time of their smaller launches, where the two-wave build
+// stays faster (C3 1/2 and 1/4 shards, 8 and 4 rounds: 172-185 / 114 ms vs 202-206 / 131 ms lean;
+// profiles/r06k_lean_rounds_ab.log), so they take it from 12 rounds on, other scenes from 3.
 bool lean_fits(nart_ctx* ctx, const RenderArgs& a) {
     if (ctx->variant != 0 || !ctx->lean || !rq_fits(ctx)) return false;
-    return launch_rounds(ctx, a.n_slots) >= 3.0;
+    const double from = (ctx->features & FT_GLASS) ? 12.0 : 3.0;
+    return launch_rounds(ctx, a.n_slots) >= env_num("NART_LEAN_ROUNDS", from);
 }
 
 int dispatch_megakernel(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
