@@ -64,7 +64,7 @@ def nested_scene(built, tmp_path_factory):
 def test_glass_sphere_specialised(gpu, glass_scene, w, h, spp):
     a, b, feats, build, sched = _both(glass_scene, _params(glass_scene, w, h, spp))
     assert feats == FM_GLASS and build == FM_GLASS, (hex(feats), hex(build))
-    assert "specialized" in sched, sched
+    assert "specialized" in sched and "lean" not in sched, sched
     assert _same_bits(a, b)
 
 
@@ -81,7 +81,8 @@ def test_glass_sphere_lean_build(gpu, glass_scene, monkeypatch, lds_levels):
     levels most pushes of the 14-level BVH go to the columns.  Same bits as the generic build."""
     if lds_levels:
         monkeypatch.setenv("NART_LEAN_STACK", lds_levels)
-    a, b, feats, build, sched = _both(glass_scene, _params(glass_scene, 1280, 720, 2))
+    # a whole 1080p frame: 16 rounds of resident waves (glass scenes go lean from 12, render.hip lean_fits)
+    a, b, feats, build, sched = _both(glass_scene, _params(glass_scene, 1920, 1080, 1))
     assert build == FM_GLASS and "lean" in sched, (hex(build), sched)
     assert _same_bits(a, b)
 
