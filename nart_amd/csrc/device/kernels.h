@@ -1026,15 +1026,18 @@ NHD size_t rq_lds_bytes(uint32_t stack_depth, uint32_t block) {
 // blocks (12 waves per CU) at three waves per SIMD; only for scenes whose specialised build fits
 // 168 VGPRs and whose traversal stack fits the block's LDS (render.hip lean_fits).
 #define RQ_BLOCK_OF(COUNT, WV) ((COUNT) ? 256 : ((WV) == 3 ? 768 : NART_RQ_BLOCK))
-template <bool EXT, bool COUNT, bool ENV, uint32_t FM = FT_ALL, int WV = 2>
+//
+// PR = false (with WV = 3): the lean build proper.  PR = true keeps the small-shard schedule's code
+// (priority lanes, speculative pairs, raised issue priority) at three waves per SIMD.
+template <bool EXT, bool COUNT, bool ENV, uint32_t FM = FT_ALL, int WV = 2, bool PR = true>
 __global__ __launch_bounds__(RQ_BLOCK_OF(COUNT, WV), COUNT ? 1 : (WV == 3 ? 3 : NART_RENDER_WAVES)) void k_render_rq(DScene S, RenderArgs A) {
     // priority lanes, speculative groups and raised issue priority: small-shard schedules only
-    const uint32_t rq_prio = WV == 3 ? 0u : A.rq_prio, rq_pairs = WV == 3 ? 0u : A.rq_pairs;
+    const uint32_t rq_prio = PR ? A.rq_prio : 0u, rq_pairs = PR ? A.rq_pairs : 0u;
     // a lean build whose shading needs more than Lambert lobes and area lights fits 168 VGPRs only
     // without the paired sample reads and with the traced ray re-formed per phase (below); the
     // Lambert-only build keeps both (132 -> 164 VGPRs, still three waves)
     constexpr bool TIGHT = WV == 3 && (FM & ~(FT_LAMBERT | FT_DISK | FT_RING)) != 0u;
-    const uint32_t rq_setprio = WV == 3 ? 0u : A.rq_setprio;
+    const uint32_t rq_setprio = PR ? A.rq_setprio : 0u;
     extern __shared__ __attribute__((aligned(16))) int s_dyn[];
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6;

@@ -598,12 +598,13 @@ __global__ void k_build_queue(const uint32_t* top, const uint32_t* rest, uint32_
     } else if (p >= g && quad) {
         queue[p] = rest[(64u - kk - 2u) * W + (p - g)];
     } else if (p < g && half) {
-        // half: only the first 4 waves of each 8-wave block hold costly pixels (2k each), so each
-        // SIMD has one priority wave and one other wave
-        const uint32_t w = p / 64u, j = p % 64u, b = w / 8u, i = w % 8u, k2 = 2u * kk;
+        // half = BW, the waves of a ray-queue block (8 or 12: PB = 2 or 3 per SIMD): only its first 4
+        // waves hold costly pixels (PB k each), so each SIMD has one priority wave
+        const uint32_t BW = half, PB = BW / 4u;
+        const uint32_t w = p / 64u, j = p % 64u, b = w / BW, i = w % BW, k2 = PB * kk;
         const uint32_t pw = b * 4u + i;  // priority wave index
-        const uint32_t roff = b * 8u * (64u - kk) + (i < 4u ? i * (64u - k2) : 4u * (64u - k2) + (i - 4u) * 64u);
-        if (i < 4u && j < k2) queue[p] = top[(j / per) * (W / 2u) + pw] | prio | (pairs ? RQ_PAIR_BIT : 0u);
+        const uint32_t roff = b * BW * (64u - kk) + (i < 4u ? i * (64u - k2) : 4u * (64u - k2) + (i - 4u) * 64u);
+        if (i < 4u && j < k2) queue[p] = top[(j / per) * (W / PB) + pw] | prio | (pairs ? RQ_PAIR_BIT : 0u);
         else queue[p] = rest[roff + (i < 4u ? j - k2 : j)];
     } else if (p < g) {
         const uint32_t w = p / 64u, j = p % 64u;
@@ -679,10 +680,10 @@ int sort_groups_by_cost(nart_ctx* ctx, uint32_t n, uint32_t* out, hipStream_t st
 
 uint32_t lean_stack(const nart_ctx* ctx);
 
-template <bool EXT, bool COUNT, bool ENV, uint32_t FM = FT_ALL, int WV = 2>
+template <bool EXT, bool COUNT, bool ENV, uint32_t FM = FT_ALL, int WV = 2, bool PR = true>
 int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
     auto kern = k_render<EXT, COUNT, ENV>;
-    auto kern_rq = k_render_rq<EXT, COUNT, ENV, FM, WV>;
+    auto kern_rq = k_render_rq<EXT, COUNT, ENV, FM, WV, PR>;
     constexpr uint32_t RQB = RQ_BLOCK_OF(COUNT, WV);  // ray-queue block (kernels.h)
     RenderArgs a = a_in;
     if (EXT) {
@@ -715,7 +716,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
     const bool rq = ctx->variant == 0 && rq_fits(ctx);
     ctx->fm_used = rq ? FM : FT_ALL;
     if (rq && FM != FT_ALL) ctx->sched |= NART_SCHED_SPECIALIZED;
-    if (rq && WV == 3) ctx->sched |= NART_SCHED_LEAN;
+    if (rq && WV == 3 && !PR) ctx->sched |= NART_SCHED_LEAN;
     // camera rays first, coherently (k_primary; leaving them to the path kernel measured C3 470 vs
     // 407 ms per frame, profiles/r02h_env_ab.log)
     const bool primary = true;
@@ -813,11 +814,35 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
             const dim3 eg((n + 255) / 256);
             // costly pixels per first-round wave: few when the shard is small (their serial chains
             // bound the frame), all 64 (packed, launched first) when there are many rounds
-            // the costly pixels on one wave per SIMD (NART_RQ_HALF=0: dealt over every wave; see below)
-            const bool half_want = rq && env_num("NART_RQ_HALF", 1.0) != 0.0;
-            // measured on C3 shards of 1/2, 1/4, 1/8 of the frame; with half_want 12 (2 x 12 on each
-            // priority wave): C3 1/8 shard mean of the 8 ranks 4/6/8/12/14/16: 95.2/88.8/81.4/80.9/81.3/81.6 ms
-            uint32_t k = R >= 3.0 ? 32u : (half_want ? 12u : 8u);
+            // Priority lanes for the costly pixels in the ray-queue kernel (NART_RQ_PRIO=0: off, 2:
+            // also on launches of >= 3 rounds), run as speculative lane groups of Q lanes
+            // (NART_RQ_PAIRS: 0 one lane per pixel, 1 or 2 pairs, 4 groups of four).  Only small
+            // shards (< 3 rounds of resident waves), whose time is their costliest pixels' chains: on
+            // throughput-bound launches the priority breaks and the speculative duplicates cost
+            // throughput (1/2 C3 shard 238 -> 249 ms, C4 batches 3175 -> 3381 ms with them on)
+            const int prio_env = (int)env_num("NART_RQ_PRIO", 1.0);
+            const bool prio_on = prio_env == 2 || (prio_env == 1 && R < q_rounds);
+            const int pe = (int)env_num("NART_RQ_PAIRS", NART_RQ_GROUP_LANES);
+            const uint32_t Q = pe <= 0 ? 0u : (pe >= 4 ? 4u : 2u);
+            // (the lean build has no priority lanes: it runs only where prio_on is false anyway)
+            const uint32_t pbit = (rq && prio_on && PR) ? RQ_PRIO_BIT : 0u;
+            // Half waves (default): the costly pixels only on the first 4 waves of each ray-queue
+            // block (8 or 12 waves), PB = 2 or 3 shares each -- one such wave per SIMD -- and those
+            // waves at a raised issue priority (s_setprio 2, NART_RQ_SETPRIO) while they hold priority
+            // work, so the SIMD's other waves fill their stalls instead of sharing issue with them.
+            // C3 1/8 shard, every rank: mean 84.2 -> 80.9 ms, worst 87-92 -> 86.0 ms
+            // (profiles/r05h_chain_schedule_ab.log).  NART_RQ_HALF=0: dealt over every wave.
+            const uint32_t BW = RQB / 64u, PB = BW / 4u;
+            // costly pixels per first-round wave: few when the shard is small (their serial chains
+            // bound the frame), all 64 (packed, launched first) when there are many rounds.  C3 1/8
+            // shard, mean of the 8 ranks with half waves at k = 4/6/8/12/14/16 per two-wave block
+            // share: 95.2/88.8/81.4/80.9/81.3/81.6 ms; three-wave blocks keep the same number of
+            // costly pixels (k W constant: 8 per share).  The half layout is settled first, so a
+            // configuration it does not fit falls back to k = 8 dealt over every wave.
+            const uint32_t k_half = PB == 2u ? 12u : 8u;
+            const bool half = pbit && rq && env_num("NART_RQ_HALF", 1.0) != 0.0 && (W % BW) == 0u && R < 3.0 &&
+                              PB * ((Q && Q * k_half <= 64u) ? Q : 1u) * k_half <= 64u;
+            uint32_t k = R >= 3.0 ? 32u : (half ? k_half : 8u);
             // ray-queue kernel: wave-group refill from 6 rounds of resident waves (C3 1/2 shard, 8
             // rounds: 241 -> 235 ms; C4 batches, ~9 rounds: 1385 -> 1566 Msamples/s).  Below that a
             // wave of costly groups outlasts the rest (1/4 shard, 4 rounds: 146 -> 211 ms), and
@@ -907,34 +932,16 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
                 tmp = ctx->cap_sort_tmp;
                 HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->d_sort_tmp, tmp, ctx->d_keys[0], ctx->d_keys[1],
                                                           ctx->d_cost, ctx->d_vals[0], (int)n, 0, 1, st));
-                // priority lanes for the costly pixels in the ray-queue kernel (NART_RQ_PRIO=0: off,
-                // 2: also on launches of >= 3 rounds), run as speculative lane pairs
-                // (NART_RQ_PAIRS=0: one lane per pixel).  Only small shards (< 3 rounds of
-                // resident waves), whose time is their costliest pixels' chains: on throughput-bound
-                // launches the priority breaks and the speculative duplicates cost throughput
-                // (1/2 C3 shard 238 -> 249 ms, C4 batches 3175 -> 3381 ms with them on)
-                const int prio_env = (int)env_num("NART_RQ_PRIO", 1.0);
-                const bool prio_on = prio_env == 2 || (prio_env == 1 && R < q_rounds);
-                // NART_RQ_PAIRS: lanes per costly pixel (0 off; 1 or 2 pairs; 4 groups of four)
-                const int pe = (int)env_num("NART_RQ_PAIRS", NART_RQ_GROUP_LANES);
-                const uint32_t Q = pe <= 0 ? 0u : (pe >= 4 ? 4u : 2u);
-                // (the lean build has no priority lanes: it runs only where prio_on is false anyway)
-                const uint32_t pbit = (rq && prio_on && WV != 3) ? RQ_PRIO_BIT : 0u;
                 const uint32_t pairs = (pbit && Q && Q * k <= 64u) ? Q : 0u;
+                // (re-checked: NART_QUEUE_K may have changed k)
+                const bool hw = half && PB * (pairs ? pairs : 1u) * k <= 64u;
                 // NART_RQ_QUAD (A/B): each first-round wave's costliest pixel gets four lanes
                 const bool quad = pbit && pairs == 2u && 2u * k + 2u <= 64u && env_num("NART_RQ_QUAD", 0.0) != 0.0;
                 const uint32_t qlen = n + (pairs ? (pairs - 1u) * k * W : 0u) + (quad ? 2u * W : 0u);
-                // Half waves (default): the costly pixels on the first 4 waves of each 8-wave block,
-                // 2k each -- one such wave per SIMD -- and those waves at a raised issue priority
-                // (s_setprio 2, NART_RQ_SETPRIO) while they hold priority work, so the other wave
-                // of the SIMD fills their stalls instead of sharing issue with them.  C3 1/8 shard,
-                // every rank: mean 84.2 -> 80.9 ms, worst 87-92 -> 86.0 ms
-                // (profiles/r05h_chain_schedule_ab.log)
-                const bool half = pbit && half_want && (W % 8u) == 0u && 2u * (pairs ? pairs : 1u) * k <= 64u;
                 hipLaunchKernelGGL(k_build_queue, dim3((qlen + 255) / 256), block, 0, st, ctx->d_vals[1], ctx->d_vals[0],
-                                   n, W, k, pbit, pairs, half ? 1u : 0u, quad ? 1u : 0u, ctx->d_queue);
-                b.rq_setprio = pbit ? (uint32_t)std::max(0.0, env_num("NART_RQ_SETPRIO", half ? 1.0 : 0.0)) : 0u;
-                if (half) ctx->sched |= NART_SCHED_HALF_WAVES;
+                                   n, W, k, pbit, pairs, hw && !quad ? BW : 0u, quad ? 1u : 0u, ctx->d_queue);
+                b.rq_setprio = pbit ? (uint32_t)std::max(0.0, env_num("NART_RQ_SETPRIO", hw ? 1.0 : 0.0)) : 0u;
+                if (hw && !quad) ctx->sched |= NART_SCHED_HALF_WAVES;
                 b.rq_prio = pbit ? 1u : 0u;
                 b.rq_pairs = pairs;
                 b.qlen = qlen;
@@ -1021,15 +1028,18 @@ int dispatch_megakernel(nart_ctx* ctx, const RenderArgs& a, hipStream_t st) {
     auto covers = [f](uint32_t m) { return (f & ~m) == 0u; };
     if (ctx->specialize && !ctx->counters && a.bounces <= ILIST_REG) {
         if (!ctx->has_env && covers(FM_DIFFUSE)) {
-            if (lean_fits(ctx, a)) return launch_render<false, false, false, FM_DIFFUSE, 3>(ctx, a, st);
+            if (lean_fits(ctx, a)) return launch_render<false, false, false, FM_DIFFUSE, 3, false>(ctx, a, st);
             return launch_render<false, false, false, FM_DIFFUSE>(ctx, a, st);
         }
         if (!ctx->has_env && covers(FM_GLASS)) {
-            if (lean_fits(ctx, a)) return launch_render<false, false, false, FM_GLASS, 3>(ctx, a, st);
+            if (lean_fits(ctx, a)) return launch_render<false, false, false, FM_GLASS, 3, false>(ctx, a, st);
+            // (small shards keep two waves per SIMD: the priority-lane build at three, 168 VGPRs with
+            // 14 spilled, measured C3 1/8 shards worst 83-85 vs 79-81 ms, mean 79.5-79.8 vs 75.9-76.0;
+            // profiles/r06l_three_wave_prio_ab.log)
             return launch_render<false, false, false, FM_GLASS>(ctx, a, st);
         }
         if (ctx->has_env && covers(FM_ENVTEX)) {
-            if (lean_fits(ctx, a)) return launch_render<false, false, true, FM_ENVTEX, 3>(ctx, a, st);
+            if (lean_fits(ctx, a)) return launch_render<false, false, true, FM_ENVTEX, 3, false>(ctx, a, st);
             return launch_render<false, false, true, FM_ENVTEX>(ctx, a, st);
         }
     }
