@@ -210,9 +210,19 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
     SlotSO so;
     const float2* smp = nullptr;
     float4* out = nullptr;
-    // the lane's next LatinSquare sample, loaded when the current one starts: a sample's first
-    // iteration used to wait for its own load, and a wave waits whenever any lane starts a sample
-    float2 nsm = make_float2(0.f, 0.f);
+    // The lane's next LatinSquare samples.  Pixel-major rows (stride 1): two samples per 16-B load,
+    // issued when the odd sample of the previous pair starts -- so a sample never waits for its own
+    // load, and each read of a line no other lane shares serves two samples (the single 8-B loads
+    // re-fetched a lane's line for every sample once other lanes' lines and the sky's texels had
+    // evicted it: 212 GB fetched per C5 launch for 17 GB of samples; with no sample loads at all
+    // the launch fetched 0.4 GB, profiles/r06m_volume_ablation.log).  Other layouts: one sample
+    // ahead, in nq.xy.
+    float4 nq = make_float4(0.f, 0.f, 0.f, 0.f);
+    bool pairs = false;
+    // Results of pixel-major rows go out four at a time (64 contiguous bytes per lane, one line
+    // sector written whole instead of four partial 16-B writes: 80 GB written per C5 launch for
+    // 34 GB of results), staged in s_out[k][thread]
+    __shared__ float4 s_outq[4][256];
     auto take = [&](uint32_t sl) {
         slot = sl;
         const uint32_t xy = A.slot_xy[sl];
@@ -224,11 +234,26 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
         out = A.Lout + so.first;
     };
     take(slot);
-    nsm = smp[0];
+    pairs = so.stride == 1u && (so.first & 3u) == 0u && (A.spp & 3u) == 0u;
+    if (pairs) nq = reinterpret_cast<const float4*>(smp)[0];
+    else nq = make_float4(smp[0].x, smp[0].y, 0.f, 0.f);
     const DMedium& m = S.medium;
     const f3 beta = F3(1.f, 1.f, 1.f);
     enum { P_SAMPLE, P_RAY, P_MAJ, P_COLL, P_ESC, P_SCAT };
     uint32_t work = 0, s = 0, bounce = 0;
+    // a sample's Li_alpha: staged and written in fours (pixel-major rows), else at once
+    auto emit = [&](float4 v) {
+        if (!pairs) {
+            out[(size_t)s * so.stride] = v;
+            return;
+        }
+        s_outq[s & 3u][threadIdx.x] = v;
+        if ((s & 3u) == 3u) {
+            float4* o4 = out + (s & ~3u);
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) o4[j] = s_outq[j][threadIdx.x];
+        }
+    };
     int ph = P_SAMPLE;
     f3 o = F3(0.f, 0.f, 0.f), d = o, ro = o, rd = o, L = o;
     float uMode = 0.f, sigma = 1.f, tMin = 0.f, t1 = 0.f;
@@ -261,14 +286,22 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
                 }
             }
             L = add(L, mul(Le, beta));
-            out[(size_t)s * so.stride] = make_float4(L.x, L.y, L.z, 1.f);
+            emit(make_float4(L.x, L.y, L.z, 1.f));
             ++s;
             ph = P_SAMPLE;
         }
         if (ph == P_SAMPLE) {
             if (s >= A.spp) break;
-            const float2 sm = nsm;
-            nsm = smp[(size_t)(s + 1u < A.spp ? s + 1u : s) * so.stride];
+            float2 sm;
+            if (pairs) {
+                sm = (s & 1u) ? make_float2(nq.z, nq.w) : make_float2(nq.x, nq.y);
+                // the odd sample of a pair starts: load the next pair (the last pair reloads itself)
+                if (s & 1u) nq = reinterpret_cast<const float4*>(smp)[(s + 1u < A.spp ? s + 1u : s - 1u) >> 1];
+            } else {
+                sm = make_float2(nq.x, nq.y);
+                const float2 n1 = smp[(size_t)(s + 1u < A.spp ? s + 1u : s) * so.stride];
+                nq = make_float4(n1.x, n1.y, 0.f, 0.f);
+            }
             const Ray r = cast_ray(S, F2(sm.x, sm.y), A.W, A.H, px, py);
             o = r.o;
             d = r.d;
@@ -360,7 +393,7 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
             }
         }
         if (finish) {
-            out[(size_t)s * so.stride] = make_float4(L.x, L.y, L.z, 1.f);
+            emit(make_float4(L.x, L.y, L.z, 1.f));
             ++s;
             ph = P_SAMPLE;
         }

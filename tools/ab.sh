@@ -8,7 +8,7 @@ R=$(pwd)
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   mkdir -p $OUT/$name
-  timeout -k 10 300 /opt/rocm/bin/hipcc --offload-arch=gfx950 -fhip-fp32-correctly-rounded-divide-sqrt -std=c++17 -O3 -fPIC \
+  timeout -k 10 300 /opt/rocm/bin/hipcc --offload-arch=gfx950 -fhip-fp32-correctly-rounded-divide-sqrt -fno-slp-vectorize -std=c++17 -O3 -fPIC \
     -ffp-contract=off -fno-fast-math -w $flags -shared -o $OUT/$name/libnart_hip.so nart_amd/csrc/render.hip \
     nart_amd/csrc/host/bvh_build.cpp -L$R/nart_amd/lib -lnart_scene -Wl,-rpath,$R/nart_amd/lib || exit 1
   echo "== $name ($flags)"

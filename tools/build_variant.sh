@@ -6,7 +6,7 @@
 NAME=$1; FLAGS=$2
 R=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p "$R/abbuild/$NAME"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -fhip-fp32-correctly-rounded-divide-sqrt -std=c++17 -O3 -fPIC \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -fhip-fp32-correctly-rounded-divide-sqrt -fno-slp-vectorize -std=c++17 -O3 -fPIC \
   -ffp-contract=off -fno-fast-math -w $FLAGS -shared -o "$R/abbuild/$NAME/libnart_hip.so" \
   "$R/nart_amd/csrc/render.hip" "$R/nart_amd/csrc/host/bvh_build.cpp" -L"$R/nart_amd/lib" -lnart_scene \
   -Wl,-rpath,'$ORIGIN/../../nart_amd/lib'
