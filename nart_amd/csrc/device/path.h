@@ -579,6 +579,8 @@ ND float half_to_float(uint16_t h) {  // Imath half -> float (exact)
     }
     return __uint_as_float(v);
 }
+// (the texel's RGBA halves as one 8-B load; a non-temporal load for the volume kernel's sky lookups
+// measured slower, 81.7 vs 79.4 ms, with the same fetch: profiles/r06o_sky_nt_ab.log)
 ND f3 tex_fetch(const DScene& S, int tex, float su, float sv, int rough) {  // texturepattern.cpp:172-187
     const DTexture& t = cst(S.texs)[tex];
     float u = gmin(gmax(su, 0.0001f), 0.9999f);
@@ -586,7 +588,10 @@ ND f3 tex_fetch(const DScene& S, int tex, float su, float sv, int rough) {  // t
     int iu = (int)((float)t.w * u);
     int iv = (int)((float)t.h * v);
     const uint16_t* px = S.tex_pool + t.offset + ((uint64_t)iv * t.w + (uint64_t)iu) * 4;
-    float rr = half_to_float(px[0]), gg = half_to_float(px[1]), bb = half_to_float(px[2]);
+    const unsigned long long* p8 = reinterpret_cast<const unsigned long long*>(px);
+    const unsigned long long q = *p8;
+    float rr = half_to_float((uint16_t)(q & 0xFFFFu)), gg = half_to_float((uint16_t)((q >> 16) & 0xFFFFu)),
+          bb = half_to_float((uint16_t)((q >> 32) & 0xFFFFu));
     if (rough) { rr *= rr; gg *= gg; bb *= bb; }
     return F3(rr, gg, bb);
 }
