@@ -19,5 +19,5 @@ run() {  # name, rocprofv3 options...
 run trace --kernel-trace --stats
 run fetch --pmc FETCH_SIZE
 run write --pmc WRITE_SIZE
-run sq --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_SALU SQ_ACTIVE_INST_LDS
+run sq --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_ACTIVE_INST_LDS
 echo profile-done

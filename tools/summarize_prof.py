@@ -25,10 +25,11 @@ def _key(name):
 
 
 def waves_per_simd(vgpr, lds=None):
-    """Resident waves per SIMD the kernel's registers (and LDS, 160 KiB per CU) allow: 512 VGPRs
-    per SIMD lane in 8-register granules, at most 8 waves."""
+    """Resident waves per SIMD the kernel's registers allow: 512 VGPRs per SIMD lane in 8-register
+    granules, at most 8 waves.  rocprofv3's VGPR_Count is in units of two registers on gfx950
+    (k_render_rq's lean build: 84 for 163 VGPRs, kernel descriptor; k_primary: 60 for 113)."""
     try:
-        v = int(vgpr)
+        v = 2 * int(vgpr)
     except (TypeError, ValueError):
         return None
     v = max(8, (v + 7) // 8 * 8)
@@ -87,10 +88,10 @@ def main(src, tag, config="1920x1080x256"):
             e["wait_any"] = top.get("SQ_WAIT_ANY", 0.0) / wc
             e["wait_inst_any"] = top.get("SQ_WAIT_INST_ANY", 0.0) / wc
             # issue rate: a wave issues at most one instruction per quad-cycle (the SQ counters'
-            # unit), so (VALU + SALU issue quad-cycles) / wave quad-cycles is the wave's issue
-            # fraction; times the waves resident per SIMD it is the SIMD's issue-slot occupancy
-            if "SQ_ACTIVE_INST_SALU" in top:
-                iw = (av + top["SQ_ACTIVE_INST_SALU"]) / wc
+            # unit), so (VALU issue quad-cycles + SALU instructions) / wave quad-cycles is the wave's
+            # issue fraction; times the waves resident per SIMD it is the SIMD's issue-slot occupancy
+            if "SQ_INSTS_SALU" in top:
+                iw = (av + top["SQ_INSTS_SALU"]) / wc
                 wps = waves_per_simd(d["vgpr"], d.get("lds"))
                 e["issue_frac_wave"] = iw
                 e["waves_per_simd"] = wps
