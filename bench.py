@@ -395,11 +395,12 @@ def main():
                                   if traffic else None),
                 "lane_utilization": prof.get("lane_utilization") if prof else None,
                 "valu_busy": prof.get("valu_busy") if prof else None,
-                # issue-rate ceiling of the path kernel (the limiter that binds):
-                # (SQ_ACTIVE_INST_VALU + SQ_ACTIVE_INST_SALU) / SQ_WAVE_CYCLES per wave (quad-cycle
-                # units: one issue per wave per quad-cycle), times the resident waves per SIMD
+                # issue-rate ceiling of the path kernel: issue_frac =
+                # (SQ_ACTIVE_INST_VALU + SQ_INSTS_SALU) / SQ_WAVE_CYCLES, the fraction of a wave's
+                # issue slots (one per quad-cycle) it used; simd_valu_frac = the SIMD's VALU pipe
+                # (two wave64 instructions per quad-cycle) over its resident waves
                 "issue_frac": prof.get("issue_frac") if prof else None,
-                "issue_frac_wave": prof.get("issue_frac_wave") if prof else None,
+                "simd_valu_frac": prof.get("simd_valu_frac") if prof else None,
                 "waves_per_simd": prof.get("waves_per_simd") if prof else None,
                 "traffic_source": prof_src,
                 "kernel": "k_render_volume_sm" if p.integrator == 1 else "k_primary + k_render_rq",

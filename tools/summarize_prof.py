@@ -87,15 +87,16 @@ def main(src, tag, config="1920x1080x256"):
             e["lane_utilization"] = top.get("SQ_THREAD_CYCLES_VALU", 0.0) / (64.0 * av) if av else None
             e["wait_any"] = top.get("SQ_WAIT_ANY", 0.0) / wc
             e["wait_inst_any"] = top.get("SQ_WAIT_INST_ANY", 0.0) / wc
-            # issue rate: a wave issues at most one instruction per quad-cycle (the SQ counters'
-            # unit), so (VALU issue quad-cycles + SALU instructions) / wave quad-cycles is the wave's
-            # issue fraction; times the waves resident per SIMD it is the SIMD's issue-slot occupancy
+            # issue rate: a wave issues at most one instruction per quad-cycle (the
+            # SQ counters' unit), so issue_frac = (VALU issue quad-cycles + SALU instructions) / wave
+            # quad-cycles is the fraction of the wave's issue slots it used.  simd_valu_frac: the
+            # SIMD's VALU pipe, which takes a wave64 instruction every 2 cycles (two per quad-cycle,
+            # MI355X_MICROARCH.md), summed over the resident waves
+            wps = waves_per_simd(d["vgpr"], d.get("lds"))
+            e["waves_per_simd"] = wps
+            e["simd_valu_frac"] = min(1.0, av / wc * wps / 2.0) if wps else None
             if "SQ_INSTS_SALU" in top:
-                iw = (av + top["SQ_INSTS_SALU"]) / wc
-                wps = waves_per_simd(d["vgpr"], d.get("lds"))
-                e["issue_frac_wave"] = iw
-                e["waves_per_simd"] = wps
-                e["issue_frac"] = min(1.0, iw * wps) if wps else None
+                e["issue_frac"] = (av + top["SQ_INSTS_SALU"]) / wc
         out["kernels"][k] = e
 
     def timed(name, base):
@@ -122,7 +123,7 @@ def main(src, tag, config="1920x1080x256"):
         out["lane_utilization"] = r.get("lane_utilization")
         out["valu_busy"] = r.get("valu_busy")
         out["issue_frac"] = r.get("issue_frac")
-        out["issue_frac_wave"] = r.get("issue_frac_wave")
+        out["simd_valu_frac"] = r.get("simd_valu_frac")
         out["waves_per_simd"] = r.get("waves_per_simd")
     json.dump(out, open(os.path.join(prof, tag + "_pmc.json"), "w"), indent=1)
     # bench.py reads pmc_latest_<config>.json (and pmc_latest.json for the headline C3 config)
