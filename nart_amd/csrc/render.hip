@@ -863,7 +863,13 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
                     // glass) taken last left a tail: at 90 % of the C3 launch only 25 of 2,048
                     // waves were still running (WAVEPROF timeline).  C3 frame 445 -> 407 ms
                     // (probe included; order 1: 408, top 20 / 35 %: 408 / 408 ms)
-                    const int order = (int)env_num("NART_RQ_ORDER", 2.0);
+                    // the lean build's slower waves leave a longer tail behind the costly groups taken
+                    // late: fully cost-ordered groups (1) measured C3 227.5 vs 235-247 ms for the
+                    // costliest 10 % first (2), 250 / 245 / 260 ms for 5 / 20 / 35 %, slot order 299
+                    // (profiles/r06r_group_order_ab.log), C2 75 vs 77 ms; C4's environment-light
+                    // frame keeps 2 (4K/128: 609 vs 624 ms, r06s_group_order_c4_c2.log), as does the
+                    // two-wave build
+                    const int order = (int)env_num("NART_RQ_ORDER", WV == 3 && !ENV ? 1.0 : 2.0);
                     ctx->sched |= NART_SCHED_WAVE_GROUPS;
                     if (order == 1 || order == 2) {
                         // cost probe: the first sample of NART_PROBE_SUB (default 8) evenly spaced
