@@ -193,6 +193,8 @@ int nart_hip_set_variant(nart_ctx* ctx, int variant);
    reports the scene's mask and the mask of the build the last render launched (0x3FF = generic). */
 int nart_hip_set_specialize(nart_ctx* ctx, int mode);
 int nart_hip_scene_features(const nart_ctx* ctx, uint32_t* features, uint32_t* build);
+/* Host only (no device): the feature mask a context would derive for a scene. */
+int nart_hip_scene_features_of(const nart_scene_blob* scene, uint32_t* features);
 #define NART_FT_LAMBERT 0x1u
 #define NART_FT_SPECULAR 0x2u
 #define NART_FT_GLASS 0x4u

@@ -140,6 +140,7 @@ _HIP_SIGS = {
     "nart_hip_set_splat_mode": (ctypes.c_int, [_P, ctypes.c_int]),
     "nart_hip_set_specialize": (ctypes.c_int, [_P, ctypes.c_int]),
     "nart_hip_scene_features": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
+    "nart_hip_scene_features_of": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint32)]),
     "nart_hip_splat_thresholds": (ctypes.c_int, [ctypes.c_float, _P]),
     "nart_hip_env_search": (ctypes.c_int, [_P, ctypes.c_uint32, _P, ctypes.c_uint32, _P, _P]),
     "nart_hip_splat_lut": (ctypes.c_int, [ctypes.c_float, _P, ctypes.POINTER(ctypes.c_uint32),
@@ -335,6 +336,16 @@ class Scene:
             self.close()
         except Exception:
             pass
+
+
+def scene_features(scene):
+    """Host only: the NART_FT_* feature mask a context would derive for the scene (it selects the
+    scene-specialised path-kernel build; nart_hip_scene_features_of)."""
+    m = ctypes.c_uint32()
+    rc = hip_lib().nart_hip_scene_features_of(scene.blob, ctypes.byref(m))
+    if rc != NART_OK:
+        raise NartError(rc, "nart_hip_scene_features_of")
+    return m.value
 
 
 def shard_buckets(n_buckets_x, n_buckets, n_devices, device_index):

@@ -150,14 +150,16 @@ int upload(nart_ctx* ctx, void*& dst, const T* src, size_t count) {
 }
 
 // Feature mask of a scene (FT_*, path.h): every material kind, light kind, textured pattern and
-// normal map the scene's records hold.  A path kernel built for a mask covering it compiles only
-// that code; unknown kinds give FT_ALL (the generic build).
-uint32_t scene_features(const std::vector<DMaterial>& mats, const std::vector<DLight>& lights) {
+// normal map the scene's records hold (a glass material's normal map is ignored, as the device
+// record drops it: glassmaterial.cpp:3-9).  A path kernel built for a mask covering it compiles
+// only that code; unknown kinds give FT_ALL (the generic build).
+uint32_t scene_features(const nart_scene_blob* blob) {
     uint32_t f = 0;
-    auto ptn = [&](const DPattern& p) {
+    auto ptn = [&](const nart_pattern& p) {
         if (p.type != NART_PTN_CONSTANT) f |= FT_TEX;
     };
-    for (const DMaterial& m : mats) {
+    for (uint32_t i = 0; i < blob->num_materials; ++i) {
+        const nart_material& m = blob->materials[i];
         switch (m.type) {
             case NART_MAT_LAMBERT: f |= FT_LAMBERT; break;
             case NART_MAT_SPECULAR: f |= FT_SPECMAT; break;
@@ -166,13 +168,14 @@ uint32_t scene_features(const std::vector<DMaterial>& mats, const std::vector<DL
             case NART_MAT_PLASTIC: f |= FT_PLASTIC; break;
             default: return FT_ALL;
         }
-        for (const DPattern* p : {&m.rho_d, &m.rho_s, &m.tau, &m.eta, &m.alpha}) ptn(*p);
-        if (m.has_normal) {
+        for (const nart_pattern* p : {&m.rho_d, &m.rho_s, &m.tau, &m.eta, &m.alpha}) ptn(*p);
+        if (m.type != NART_MAT_GLASS && m.has_normal) {
             f |= FT_NMAP;
             ptn(m.normal);
         }
     }
-    for (const DLight& L : lights) {
+    for (uint32_t l = 0; l < blob->num_lights; ++l) {
+        const nart_light& L = blob->lights[l];
         switch (L.type) {
             case NART_LIGHT_DISK: f |= FT_DISK; break;
             case NART_LIGHT_RING: f |= FT_RING; break;
@@ -679,6 +682,12 @@ int sort_groups_by_cost(nart_ctx* ctx, uint32_t n, uint32_t* out, hipStream_t st
 }
 
 uint32_t lean_stack(const nart_ctx* ctx);
+// traversal-phase quorum of throughput-bound ray-queue launches: the phase ends once the wave's
+// queue is empty and at most this many lanes still trace (0/4/16/32: 134.7/123.5/123.0/129.9 vs
+// 121.6 ms at 8 in round 2)
+#ifndef NART_RQ_QUORUM
+#define NART_RQ_QUORUM 8u
+#endif
 
 template <bool EXT, bool COUNT, bool ENV, uint32_t FM = FT_ALL, int WV = 2, bool PR = true>
 int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
@@ -777,7 +786,7 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
             r2.lds_nodes = brq.lds_nodes;
             r2.prim = brq.prim;
             r2.stack_lds = skd;
-            r2.rq_quorum = R >= q_rounds ? 8u : 0u;
+            r2.rq_quorum = R >= q_rounds ? NART_RQ_QUORUM : 0u;
             const uint32_t per = RQB / 256;  // launches are counted in blocks of 256
             const uint32_t grid = (nblocks + per - 1) / per;
             const size_t threads = (size_t)grid * RQB;
@@ -1756,7 +1765,7 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     }
     if ((rc = upload(ctx, ctx->d_envs, envs.data(), envs.size()))) return bail(rc);
     if ((rc = upload(ctx, ctx->d_lights, lights.data(), lights.size()))) return bail(rc);
-    ctx->features = scene_features(mats, lights);
+    ctx->features = scene_features(blob);
     std::vector<DTexture> texs(blob->num_textures);
     size_t pool = 0;
     for (uint32_t t = 0; t < blob->num_textures; ++t) {
@@ -1887,6 +1896,12 @@ int nart_hip_set_specialize(nart_ctx* ctx, int mode) {
         c->specialize = ctx->specialize;
         c->lean = ctx->lean;
     }
+    return NART_OK;
+}
+
+int nart_hip_scene_features_of(const nart_scene_blob* scene, uint32_t* features) {
+    if (!scene || !features) return NART_E_INVALID;
+    *features = scene_features(scene);
     return NART_OK;
 }
 
