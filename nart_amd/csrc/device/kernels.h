@@ -2075,6 +2075,83 @@ __global__ __launch_bounds__(256) void k_splat_col4(SplatArgs A) {
     }
 }
 
+// k_splat_skew's per-sample steps.  skew_prep forms the W window rows' image coordinates
+// ys_k = yb + k (exact small integers) and distance terms two rows per packed instruction
+// ((ys_k + 0.5) - scy and d2 = dx2 + distY^2 are the same IEEE operations per row; ys_k + 1 is
+// ys_{k+1}) and issues the W weight-cell reads together (a read inside each row's branch waited
+// for its own LDS round trip; a row that is not hit reads a clamped, valid cell and discards it).
+template <int W>
+struct SkewPrep {
+    float ys[2 * ((W + 2) / 2)], d2[2 * ((W + 2) / 2)];
+    float4 ev[W];
+    float loy, hiy;
+    bool xhit;
+};
+template <int W>
+ND void skew_prep(SkewPrep<W>& p, float2 uv, float fx, float fy, float edgeX, float edgeY, float xsA, float xsB,
+                  float ybA, float ybB, float fw, const float4* s_lut, int lut_b0, int lut_last) {
+    constexpr int WP = (W + 2) / 2;  // row pairs covering ys_0 .. ys_W
+    const float scx = fx + uv.x, scy = fy + uv.y;
+    const float xs = scx >= edgeX ? xsB : xsA;
+    p.xhit = (scx - fw) < xs + 1.f && xs < (scx + fw);
+    const float distX = (xs + 0.5f) - scx;
+    const float dx2 = distX * distX;
+    const float yb = scy >= edgeY ? ybB : ybA;
+    p.loy = scy - fw;
+    p.hiy = scy + fw;
+#pragma unroll
+    for (int k = 0; k < WP; ++k) {
+        const nd_f2v y2 = nd_f2v{yb, yb} + nd_f2v{(float)(2 * k), (float)(2 * k + 1)};
+        const nd_f2v dy = (y2 + nd_f2v{0.5f, 0.5f}) - nd_f2v{scy, scy};
+        const nd_f2v dd = nd_f2v{dx2, dx2} + dy * dy;
+        p.ys[2 * k] = y2.x;
+        p.ys[2 * k + 1] = y2.y;
+        p.d2[2 * k] = dd.x;
+        p.d2[2 * k + 1] = dd.y;
+    }
+#pragma unroll
+    for (int k = 0; k < W; ++k) p.ev[k] = s_lut[lut_cell(p.d2[k], lut_b0, lut_last)];
+}
+// Row k is hit iff xhit && loy < ys_{k+1} && ys_k < hiy.  Both row tests are monotone in k
+// (ys_k = yb + k exactly), so every row is hit iff row 0 passes the first and row W-1 the
+// second -- all but never fails (a sample exactly on a pixel edge): the rows then accumulate
+// without per-row branches (4-5 scalar exec-mask instructions and two compares per row).
+// (A wave-uniform form of this test -- a ballot, the per-row path for the whole wave when any
+// lane misses a row -- measured slower: C5 splat 69.4-70.5 vs 68.2-68.8 ms,
+// profiles/r05r_skew_uniform_ab.log.)
+template <int W>
+ND bool skew_all_rows(const SkewPrep<W>& p) {
+    return p.xhit && p.loy < p.ys[1] && p.ys[W - 1] < p.hiy;
+}
+template <int W>
+ND void skew_add_all(const SkewPrep<W>& p, float4 L, nd_f2v (&cxy)[W], nd_f2v (&czw)[W], float (&cws)[W]) {
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        const float w = p.d2[k] >= p.ev[k].x ? p.ev[k].z : p.ev[k].y;
+        const nd_f2v w2 = nd_f2v{w, w};
+        cxy[k] += nd_f2v{L.x, L.y} * w2;
+        czw[k] += nd_f2v{L.z, L.w} * w2;
+        cws[k] += w;
+    }
+}
+template <int W>
+ND void skew_add_rows(const SkewPrep<W>& p, float4 L, nd_f2v (&cxy)[W], nd_f2v (&czw)[W], float (&cws)[W]) {
+    if (skew_all_rows(p)) {
+        skew_add_all(p, L, cxy, czw, cws);
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        if (p.xhit && p.loy < p.ys[k + 1] && p.ys[k] < p.hiy) {
+            const float w = p.d2[k] >= p.ev[k].x ? p.ev[k].z : p.ev[k].y;
+            const nd_f2v w2 = nd_f2v{w, w};
+            cxy[k] += nd_f2v{L.x, L.y} * w2;
+            czw[k] += nd_f2v{L.z, L.w} * w2;
+            cws[k] += w;
+        }
+    }
+}
+
 // Skewed-time splat over the pixel-major sample layout (sample i of bucket-local pixel q at
 // (base + q) * spp + i), one lane per tile column, LUT filter weights (power-of-two buckets).
 // AddSample (render.cpp:23-70) adds a bucket's sources to the tile in raster order; a tile pixel
@@ -2101,7 +2178,7 @@ __global__ __launch_bounds__(256) void k_splat_col4(SplatArgs A) {
 // read by both neighbours): NB times the waves for ~1/NB of the steps each, for launches whose
 // time is otherwise the waves' latency (VALU ~30 % busy at 2.7 waves per SIMD).
 template <int R, int NB>
-__global__ __launch_bounds__(256) void k_splat_skew(SplatArgs A) {
+__global__ __launch_bounds__(256, 2) void k_splat_skew(SplatArgs A) {
     constexpr int W = 2 * R + 1, NWR = 2 * R + 2;
     extern __shared__ __attribute__((aligned(16))) float4 s_dyn4[];
     float4* s_lut = s_dyn4;
@@ -2185,66 +2262,34 @@ __global__ __launch_bounds__(256) void k_splat_skew(SplatArgs A) {
     float fy = 0.f, ybA = 0.f, ybB = 0.f;  // per source row: fy, and the window's first image row
                                            // without / with the y wrap (splat_hits_fast)
     float fx = 0.f;
-    // one sample into the window rows wb .. wb+2R (splat_hits_fast + the LUT weight).  The
-    // rows' image coordinates ys_k = yb + k (exact small integers) and the distance terms are
-    // formed two rows per packed instruction: (ys_k + 0.5) - scy and d2 = dx2 + distY^2 are
-    // the same IEEE operations per row; ys_k + 1 is ys_{k+1}.
+    // one sample into the window rows wb .. wb+2R: skew_prep + skew_add_all / skew_add_rows
     auto splat_w = [&](float2 uv, float4 L) {
-        const float scx = fx + uv.x, scy = fy + uv.y;
-        const float xs = scx >= edgeX ? xsB : xsA;
-        const bool xhit = (scx - fw) < xs + 1.f && xs < (scx + fw);
-        const float distX = (xs + 0.5f) - scx;
-        const float dx2 = distX * distX;
-        const float yb = scy >= edgeY ? ybB : ybA;
-        const float loy = scy - fw, hiy = scy + fw;
-        constexpr int WP = (W + 2) / 2;  // row pairs covering ys_0 .. ys_W
-        float ys[2 * WP], d2[2 * WP];
+        SkewPrep<W> p;
+        skew_prep(p, uv, fx, fy, edgeX, edgeY, xsA, xsB, ybA, ybB, fw, s_lut, lut_b0, lut_last);
+        skew_add_rows(p, L, cxy, czw, cws);
+    };
+    // a group of PF samples: every sample's distance terms and cell reads first (one basic block,
+    // so one sample's LDS round trip overlaps the next one's arithmetic; per-sample branches had
+    // kept the scheduler to one sample at a time), then the accumulation in sample order,
+    // branch-free when every row of every sample is hit -- each accumulator receives the same
+    // products in the same order as from splat_w
+    constexpr uint32_t PF = NART_SKEW_PF;
+    constexpr uint32_t G = R >= 3 ? 2u : PF;  // samples per group (R = 3: 7 rows each, 2 waves/SIMD)
+    static_assert(PF % G == 0, "prefetch group = whole sample groups");
+    auto splat_grp = [&](const float2* uv, const float4* L) {
+        SkewPrep<W> p[G];
+        bool all = true;
 #pragma unroll
-        for (int k = 0; k < WP; ++k) {
-            const nd_f2v y2 = nd_f2v{yb, yb} + nd_f2v{(float)(2 * k), (float)(2 * k + 1)};
-            const nd_f2v dy = (y2 + nd_f2v{0.5f, 0.5f}) - nd_f2v{scy, scy};
-            const nd_f2v dd = nd_f2v{dx2, dx2} + dy * dy;
-            ys[2 * k] = y2.x;
-            ys[2 * k + 1] = y2.y;
-            d2[2 * k] = dd.x;
-            d2[2 * k + 1] = dd.y;
+        for (uint32_t u = 0; u < G; ++u) {
+            skew_prep(p[u], uv[u], fx, fy, edgeX, edgeY, xsA, xsB, ybA, ybB, fw, s_lut, lut_b0, lut_last);
+            all = all && skew_all_rows(p[u]);
         }
-        // the W weight-cell reads are issued together, before any per-row branch (a read inside
-        // each branch waited for its own LDS round trip: W dependent waits per sample); a row that
-        // is not hit reads a clamped, valid cell and discards it
-        float4 ev[W];
+        if (all) {
 #pragma unroll
-        for (int k = 0; k < W; ++k) ev[k] = s_lut[lut_cell(d2[k], lut_b0, lut_last)];
-        // Row k is hit iff xhit && loy < ys_{k+1} && ys_k < hiy.  Both row tests are monotone in k
-        // (ys_k = yb + k exactly), so every row is hit iff row 0 passes the first and row W-1 the
-        // second -- all but never fails (a sample exactly on a pixel edge): the rows then accumulate
-        // without per-row branches (4-5 scalar exec-mask instructions and two compares per row).
-        // (A wave-uniform form of this test -- a ballot, the per-row path for the whole wave when any
-        // lane misses a row -- measured slower: C5 splat 69.4-70.5 vs 68.2-68.8 ms,
-        // profiles/r05r_skew_uniform_ab.log.)
-        if (xhit && loy < ys[1] && ys[W - 1] < hiy) {
-#pragma unroll
-            for (int k = 0; k < W; ++k) {
-                const float4 e = ev[k];
-                const float w = d2[k] >= e.x ? e.z : e.y;
-                const nd_f2v w2 = nd_f2v{w, w};
-                cxy[k] += nd_f2v{L.x, L.y} * w2;
-                czw[k] += nd_f2v{L.z, L.w} * w2;
-                cws[k] += w;
-            }
+            for (uint32_t u = 0; u < G; ++u) skew_add_all(p[u], L[u], cxy, czw, cws);
         } else {
 #pragma unroll
-            for (int k = 0; k < W; ++k) {
-                const bool hit = xhit && loy < ys[k + 1] && ys[k] < hiy;
-                if (hit) {
-                    const float4 e = ev[k];
-                    const float w = d2[k] >= e.x ? e.z : e.y;
-                    const nd_f2v w2 = nd_f2v{w, w};
-                    cxy[k] += nd_f2v{L.x, L.y} * w2;
-                    czw[k] += nd_f2v{L.z, L.w} * w2;
-                    cws[k] += w;
-                }
-            }
+            for (uint32_t u = 0; u < G; ++u) skew_add_rows(p[u], L[u], cxy, czw, cws);
         }
     };
     auto source_pass = [&](int sy, int sx) {  // every sample of bucket-local pixel (sx, sy)
@@ -2252,7 +2297,6 @@ __global__ __launch_bounds__(256) void k_splat_skew(SplatArgs A) {
         const float2* sp = A.samples + first;
         const float4* lp = A.Lout + first;
         fx = (float)(x0 + (uint32_t)sx + A.fb);
-        constexpr uint32_t PF = NART_SKEW_PF;
         uint32_t i = 0;
         float2 nu[PF];
         float4 nL[PF];
@@ -2279,7 +2323,7 @@ __global__ __launch_bounds__(256) void k_splat_skew(SplatArgs A) {
                 }
             }
 #pragma unroll
-            for (uint32_t u = 0; u < PF; ++u) splat_w(uv[u], Lv[u]);
+            for (uint32_t u = 0; u < PF; u += G) splat_grp(uv + u, Lv + u);
         }
         for (; i < A.spp; ++i) splat_w(sp[i], lp[i]);
     };
