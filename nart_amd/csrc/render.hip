@@ -854,9 +854,12 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
             uint32_t k = R >= 3.0 ? 32u : (half ? k_half : 8u);
             // ray-queue kernel: wave-group refill from 6 rounds of resident waves (C3 1/2 shard, 8
             // rounds: 241 -> 235 ms; C4 batches, ~9 rounds: 1385 -> 1566 Msamples/s).  Below that a
-            // wave of costly groups outlasts the rest (1/4 shard, 4 rounds: 146 -> 211 ms), and
-            // the probe-ordered pixel queue with priority lanes stays
-            const double g_rounds = 6.0;
+            // wave of costly groups outlasts the rest (1/4 shard, 4 rounds: 146 -> 211 ms; with the
+            // groups cost-ordered still 156 vs 114 ms), and the probe-ordered pixel queue with
+            // priority lanes stays.  The lean build (from 3 rounds where it runs: scenes without
+            // glass) takes groups from there: C2 1/4 shard 32.2 -> 27.9 ms
+            // (profiles/r06x_mid_shards.log)
+            const double g_rounds = WV == 3 ? 3.0 : 6.0;
             if (R >= (rq ? g_rounds : 12.0) && mode == 2 && !env_opt("NART_QUEUE_K")) {
                 // many rounds: the slot order (costly waves interleaved with cheap ones in time)
                 // measured faster than any reordering; no probe.  The ray-queue kernel runs it on
@@ -876,9 +879,10 @@ int launch_render(nart_ctx* ctx, const RenderArgs& a_in, hipStream_t st) {
                     // late: fully cost-ordered groups (1) measured C3 227.5 vs 235-247 ms for the
                     // costliest 10 % first (2), 250 / 245 / 260 ms for 5 / 20 / 35 %, slot order 299
                     // (profiles/r06r_group_order_ab.log), C2 75 vs 77 ms; C4's environment-light
-                    // frame keeps 2 (4K/128: 609 vs 624 ms, r06s_group_order_c4_c2.log), as does the
-                    // two-wave build
-                    const int order = (int)env_num("NART_RQ_ORDER", WV == 3 && !ENV ? 1.0 : 2.0);
+                    // frame keeps 2 (4K/128: 609 vs 624 ms, r06s_group_order_c4_c2.log).  The two-wave
+                    // build's launches of 6-12 rounds (C3 1/2 shard, chain-bound) also take 1: worst
+                    // rank 183-184 -> 167-169 ms (profiles/r06x_mid_shards.log)
+                    const int order = (int)env_num("NART_RQ_ORDER", !ENV ? 1.0 : 2.0);
                     ctx->sched |= NART_SCHED_WAVE_GROUPS;
                     if (order == 1 || order == 2) {
                         // cost probe: the first sample of NART_PROBE_SUB (default 8) evenly spaced
