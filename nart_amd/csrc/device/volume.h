@@ -210,14 +210,14 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
     SlotSO so;
     const float2* smp = nullptr;
     float4* out = nullptr;
-    // The lane's next LatinSquare samples.  Pixel-major rows (stride 1): two samples per 16-B load,
-    // issued when the odd sample of the previous pair starts -- so a sample never waits for its own
-    // load, and each read of a line no other lane shares serves two samples (the single 8-B loads
-    // re-fetched a lane's line for every sample once other lanes' lines and the sky's texels had
-    // evicted it: 212 GB fetched per C5 launch for 17 GB of samples; with no sample loads at all
-    // the launch fetched 0.4 GB, profiles/r06m_volume_ablation.log).  Other layouts: one sample
-    // ahead, in nq.xy.
-    float4 nq = make_float4(0.f, 0.f, 0.f, 0.f);
+    // The lane's next LatinSquare samples.  Pixel-major rows (stride 1): four samples per 32-B load
+    // pair, issued when the last sample of the previous quad starts -- so a sample never waits for
+    // its own load, and each read of a line no other lane shares serves four samples (the single
+    // 8-B loads re-fetched a lane's line for every sample once other lanes' lines and the sky's
+    // texels had evicted it: 212 GB fetched per C5 launch for 17 GB of samples; with no sample
+    // loads at all the launch fetched 0.4 GB, profiles/r06m_volume_ablation.log; pairs: 91 GB).
+    // Other layouts: one sample ahead, in nq.xy.
+    float4 nq = make_float4(0.f, 0.f, 0.f, 0.f), nq1 = nq;
     bool pairs = false;
     // Results of pixel-major rows go out four at a time (64 contiguous bytes per lane, one line
     // sector written whole instead of four partial 16-B writes: 80 GB written per C5 launch for
@@ -235,8 +235,12 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
     };
     take(slot);
     pairs = so.stride == 1u && (so.first & 3u) == 0u && (A.spp & 3u) == 0u;
-    if (pairs) nq = reinterpret_cast<const float4*>(smp)[0];
-    else nq = make_float4(smp[0].x, smp[0].y, 0.f, 0.f);
+    if (pairs) {
+        nq = reinterpret_cast<const float4*>(smp)[0];
+        nq1 = reinterpret_cast<const float4*>(smp)[1];
+    } else {
+        nq = make_float4(smp[0].x, smp[0].y, 0.f, 0.f);
+    }
     const DMedium& m = S.medium;
     const f3 beta = F3(1.f, 1.f, 1.f);
     enum { P_SAMPLE, P_RAY, P_MAJ, P_COLL, P_ESC, P_SCAT };
@@ -294,9 +298,14 @@ __global__ __launch_bounds__(256, WV) void k_render_volume_sm(DScene S, RenderAr
             if (s >= A.spp) break;
             float2 sm;
             if (pairs) {
-                sm = (s & 1u) ? make_float2(nq.z, nq.w) : make_float2(nq.x, nq.y);
-                // the odd sample of a pair starts: load the next pair (the last pair reloads itself)
-                if (s & 1u) nq = reinterpret_cast<const float4*>(smp)[(s + 1u < A.spp ? s + 1u : s - 1u) >> 1];
+                const float4 h = (s & 2u) ? nq1 : nq;
+                sm = (s & 1u) ? make_float2(h.z, h.w) : make_float2(h.x, h.y);
+                // the last sample of a quad starts: load the next quad (the last quad reloads itself)
+                if ((s & 3u) == 3u) {
+                    const float4* q = reinterpret_cast<const float4*>(smp) + ((s + 1u < A.spp ? s + 1u : s - 3u) >> 1);
+                    nq = q[0];
+                    nq1 = q[1];
+                }
             } else {
                 sm = make_float2(nq.x, nq.y);
                 const float2 n1 = smp[(size_t)(s + 1u < A.spp ? s + 1u : s) * so.stride];
