@@ -1038,7 +1038,11 @@ double launch_rounds(nart_ctx* ctx, uint32_t n) {
 // profiles/r06k_lean_rounds_ab.log), so they take it from 12 rounds on, other scenes from 3.
 bool lean_fits(nart_ctx* ctx, const RenderArgs& a) {
     if (ctx->variant != 0 || !ctx->lean || !rq_fits(ctx)) return false;
-    const double from = (ctx->features & FT_GLASS) ? 12.0 : 3.0;
+    // glass scenes' small launches are bound by their costly pixels' chains, which the priority
+    // lanes of the two-wave build shorten (C3 1/2, 1/4 shards: 183 / 115 ms two-wave vs 194 / 130
+    // lean); scenes without glass or an environment light take the lean build from 1.5 rounds
+    // (C2 1/8 shards, 2 rounds: mean 22.1 vs 23.9 ms, profiles/r06zg_c2_shard8.log)
+    const double from = (ctx->features & FT_GLASS) ? 12.0 : (ctx->has_env ? 3.0 : 1.5);
     return launch_rounds(ctx, a.n_slots) >= env_num("NART_LEAN_ROUNDS", from);
 }
 

@@ -95,6 +95,15 @@ def test_cornell_lean_build(gpu, cornell_scene):
     assert _same_bits(a, b)
 
 
+def test_cornell_lean_probe_queue(gpu, cornell_scene):
+    """Scenes without glass or an environment light run the lean build from 1.5 rounds of resident
+    waves (render.hip lean_fits): a 2-round Cornell frame takes it through the probe-ordered pixel
+    queue (no wave groups below 3 rounds).  Same bits as the generic build."""
+    a, b, feats, build, sched = _both(cornell_scene, _params(cornell_scene, 640, 480, 2))
+    assert build == FM_DIFFUSE and "lean" in sched and "wave_groups" not in sched, (hex(build), sched)
+    assert _same_bits(a, b)
+
+
 @pytest.mark.parametrize("w,h,spp,lean", [(384, 216, 4, False), (1280, 720, 2, True)], ids=["small", "lean"])
 def test_c4_specialised(gpu, c4_scene, w, h, spp, lean):
     a, b, feats, build, sched = _both(c4_scene, _params(c4_scene, w, h, spp))
