@@ -410,12 +410,18 @@ __global__ __launch_bounds__(256) void k_latin_draws(RenderArgs A, LatinScratch 
 #ifndef NART_LATIN_PF
 #define NART_LATIN_PF 16  // choice words (2 swaps each) loaded one batch ahead of their swaps
 #endif
-__global__ __launch_bounds__(64) void k_latin_perm(RenderArgs A, LatinScratch L) {
+// BL lanes per block, each with its own u16 column of the block's [i][BL] LDS array.  BL = 80
+// where one 64-lane block per CU is all the LDS holds (640 < spp <= 1024: 128 KiB of 160 per 64
+// lanes): the 80-lane block fills the 160 KiB, and its second wave (16 lanes) runs its own swap
+// chain on another SIMD.  The kernel is bound by one wave's instruction chain, not by lanes.
+template <uint32_t BL>
+__global__ __launch_bounds__(BL) void k_latin_perm(RenderArgs A, LatinScratch L) {
     extern __shared__ __attribute__((aligned(16))) uint16_t s_idx[];
-    const uint32_t lane = threadIdx.x, g = blockIdx.x;
-    if (g * 64u + lane >= A.n_slots) return;
+    const uint32_t slot = blockIdx.x * BL + threadIdx.x;
+    if (slot >= A.n_slots) return;
+    const uint32_t g = slot >> 6, lane = slot & 63u;
     const uint32_t n = A.spp, n2 = L.n2;
-    uint16_t* ix = s_idx + lane;
+    uint16_t* ix = s_idx + threadIdx.x;
     for (int pass = 0; pass < 2; ++pass) {
         const uint32_t* c = (pass ? L.cy : L.cx) + latin_row(g, n2, 0, lane);
         uint32_t* so = (pass ? L.sy : L.sx) + latin_row(g, n2, 0, lane);
@@ -425,7 +431,7 @@ __global__ __launch_bounds__(64) void k_latin_perm(RenderArgs A, LatinScratch L)
         uint32_t cur[PF], nxt[PF];
 #pragma unroll
         for (uint32_t u = 0; u < PF; ++u) cur[u] = c[(size_t)u * 64];
-        for (uint32_t i = 0; i < 2 * n2; ++i) ix[i * 64] = (uint16_t)i;
+        for (uint32_t i = 0; i < 2 * n2; ++i) ix[i * BL] = (uint16_t)i;
         // Full batches (all 2*PF swaps valid) load the next batch unconditionally (the choice
         // arrays carry PF padding rows), so that no branch sits between a load and its use: with
         // guarded loads the compiler waited for every outstanding load (vmcnt(0)) before each
@@ -445,18 +451,18 @@ __global__ __launch_bounds__(64) void k_latin_perm(RenderArgs A, LatinScratch L)
             if (2 * i2 >= m) {  // wave-uniform
                 uint32_t bv[2 * PF], rv[2 * PF];
 #pragma unroll
-                for (uint32_t q = 0; q < 2 * PF; ++q) bv[q] = ix[(2 * i2 + q) * 64];
+                for (uint32_t q = 0; q < 2 * PF; ++q) bv[q] = ix[(2 * i2 + q) * BL];
 #pragma unroll
                 for (uint32_t u = 0; u < PF; ++u) {
 #pragma unroll
                     for (uint32_t h = 0; h < 2; ++h) {
                         const uint32_t ci = (cur[u] >> (16 * h)) & 0xFFFFu;
-                        rv[2 * u + h] = ix[ci * 64];
-                        ix[ci * 64] = (uint16_t)bv[2 * u + h];
+                        rv[2 * u + h] = ix[ci * BL];
+                        ix[ci * BL] = (uint16_t)bv[2 * u + h];
                     }
                 }
 #pragma unroll
-                for (uint32_t q = 0; q < 2 * PF; ++q) ix[(2 * i2 + q) * 64] = (uint16_t)rv[q];
+                for (uint32_t q = 0; q < 2 * PF; ++q) ix[(2 * i2 + q) * BL] = (uint16_t)rv[q];
 #pragma unroll
                 for (uint32_t u = 0; u < PF; ++u) cur[u] = nxt[u];
                 continue;
@@ -467,9 +473,9 @@ __global__ __launch_bounds__(64) void k_latin_perm(RenderArgs A, LatinScratch L)
                 for (uint32_t h = 0; h < 2; ++h) {
                     const uint32_t i = 2 * (i2 + u) + h;
                     const uint32_t ci = (cur[u] >> (16 * h)) & 0xFFFFu;
-                    const uint16_t t = ix[i * 64];
-                    ix[i * 64] = ix[ci * 64];
-                    ix[ci * 64] = t;
+                    const uint16_t t = ix[i * BL];
+                    ix[i * BL] = ix[ci * BL];
+                    ix[ci * BL] = t;
                 }
             }
 #pragma unroll
@@ -480,14 +486,14 @@ __global__ __launch_bounds__(64) void k_latin_perm(RenderArgs A, LatinScratch L)
                 const uint32_t i = 2 * (i2 + u) + h;
                 if (i < n) {
                     const uint32_t ci = (cur[u] >> (16 * h)) & 0xFFFFu;
-                    const uint16_t t = ix[i * 64];
-                    ix[i * 64] = ix[ci * 64];
-                    ix[ci * 64] = t;
+                    const uint16_t t = ix[i * BL];
+                    ix[i * BL] = ix[ci * BL];
+                    ix[ci * BL] = t;
                 }
             }
         }
         for (uint32_t j2 = 0; j2 < n2; ++j2)
-            so[(size_t)j2 * 64] = (uint32_t)ix[2 * j2 * 64] | ((uint32_t)ix[(2 * j2 + 1) * 64] << 16);
+            so[(size_t)j2 * 64] = (uint32_t)ix[2 * j2 * BL] | ((uint32_t)ix[(2 * j2 + 1) * BL] << 16);
     }
 }
 

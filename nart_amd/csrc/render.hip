@@ -1256,7 +1256,12 @@ int launch_latin(nart_ctx* ctx, const RenderArgs& ra, hipStream_t st) {
         ls.sy = base + 3 * words;
         ls.st = base + 4 * words;
         hipLaunchKernelGGL(k_latin_draws, dim3((ra.n_slots + 255) / 256), dim3(256), 0, st, ra, ls);
-        hipLaunchKernelGGL(k_latin_perm, dim3(groups), dim3(64), (size_t)ls.n2 * 2 * 64 * sizeof(uint16_t), st, ra, ls);
+        if ((size_t)ls.n2 * 4 * 128 > 160 * 1024)  // one 64-lane block per CU: 80 lanes fill its LDS
+            hipLaunchKernelGGL(k_latin_perm<80>, dim3((ra.n_slots + 79) / 80), dim3(80),
+                               (size_t)ls.n2 * 2 * 80 * sizeof(uint16_t), st, ra, ls);
+        else
+            hipLaunchKernelGGL(k_latin_perm<64>, dim3(groups), dim3(64), (size_t)ls.n2 * 2 * 64 * sizeof(uint16_t),
+                               st, ra, ls);
         hipLaunchKernelGGL(k_latin_emit, dim3((ra.n_slots + LATIN_EMIT_SLOTS - 1) / LATIN_EMIT_SLOTS), dim3(256),
                            (size_t)ra.spp * LATIN_EMIT_SLOTS * sizeof(uint32_t), st, ra, ls);
         HIPCHK(hipGetLastError());
@@ -1657,7 +1662,9 @@ int nart_hip_create(const nart_scene_blob* blob, int device_id, nart_ctx** out) 
     if (hipFuncSetAttribute((const void*)k_latin_idx, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
         hipSuccess)
         return bail(NART_E_HIP);
-    if (hipFuncSetAttribute((const void*)k_latin_perm, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+    if (hipFuncSetAttribute((const void*)k_latin_perm<64>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+            hipSuccess ||
+        hipFuncSetAttribute((const void*)k_latin_perm<80>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
             hipSuccess ||
         hipFuncSetAttribute((const void*)k_latin_emit, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
             hipSuccess)
